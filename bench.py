@@ -1,0 +1,234 @@
+#!/usr/bin/env python3
+"""bench.py -- perft leaf nodes/s (headline) + validated moves/s on MI355X.
+
+Contract (see README / DESIGN.md):
+  python bench.py --gpus N --steps K --warmup W
+  N>1: launched by torch.distributed.run, one rank per GPU; RCCL ("nccl") for
+  the per-root-move all-reduce of leaf counts and the max-over-ranks timing.
+
+Workload (BASELINE.json configs[1]): perft(startpos, 6) under RULES_REF -- the
+reference validator's own rules (core/src/chess.rs), bit-exact -- with the
+frontier at ply 3 split into contiguous shards over the ranks.  One step = one
+full perft(startpos, 6); value = leaves of all ranks / wall time (strong
+scaling: the tree is fixed, N ranks share it).  The secondary "replay" object is
+BASELINE configs[3]: 10M synthetic seeded games x 80 ply slots replayed per
+rank (weak scaling), inputs resident in HBM, validated moves/s.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "distributed-chess_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+import numpy as np  # noqa: E402
+
+import dchess  # noqa: E402
+
+METRIC = "perft leaf nodes/sec + validated moves/sec (node), at 1/2/4/8 MI355X"
+# REF perft(startpos, d): three-way agreed (refcpu <= d4, fastcpu, GPU), tests/golden/oracle_golden.json
+REF_STARTPOS = {1: 20, 2: 400, 3: 8902, 4: 197742, 5: 4896998, 6: 120909581, 7: None}
+
+# MI355X (gfx950): 256 CUs x 4 SIMD-32 x 32 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md).
+VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+# W = 32-bit VALU lane-ops per leaf of k_count2 (SQ_INSTS_VALU x 64 / leaves), frozen from the
+# rocprofv3 PMC pass in profiles/ (see DESIGN.md "Roofline"); None until measured.
+W_COUNT2 = None
+W_REPLAY = None
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--depth", type=int, default=6)
+    ap.add_argument("--split", type=int, default=3)
+    ap.add_argument("--games", type=int, default=10_000_000, help="replay games per rank")
+    ap.add_argument("--plies", type=int, default=80)
+    ap.add_argument("--replay-steps", type=int, default=5)
+    ap.add_argument("--no-replay", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--profile-only", action="store_true", help="run the steps, print nothing (rocprof)")
+    return ap.parse_args()
+
+
+class Dist:
+    def __init__(self, want):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        if want > 1 and self.world != want:
+            raise SystemExit(f"--gpus {want} needs torch.distributed.run with {want} ranks (WORLD_SIZE={self.world})")
+        import torch
+        self.torch = torch
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            torch.cuda.set_device(self.local)
+            dist.init_process_group("nccl")
+            self.dist = dist
+
+    def sync(self):
+        if self.dist is not None:
+            self.dist.barrier()
+        if self.torch.cuda.is_available():
+            self.torch.cuda.synchronize()
+
+    def allreduce_u64(self, arr):
+        if self.dist is None:
+            return arr
+        t = self.torch.tensor(arr.astype(np.int64), device=f"cuda:{self.local}")
+        self.dist.all_reduce(t)  # RCCL over xGMI
+        return t.cpu().numpy().astype(np.uint64)
+
+    def max(self, x):
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=f"cuda:{self.local}")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+
+def perft_step(eng, d, args, pos):
+    tot, div, rm = eng.perft_shard(pos, args.depth, args.split, d.rank, d.world)
+    div = d.allreduce_u64(div)
+    return int(div.sum(dtype=np.uint64)), div, rm
+
+
+def cpu_baselines(args, threads):
+    """Reference-faithful CPU path (refcpu, the restatement of chess.rs) on a
+    bounded sample, plus the fast mailbox engine.  Test infrastructure only."""
+    import oracle_lib as O
+    out = {}
+    # refcpu brute-force perft (4096 validate_move calls per interior node)
+    t0 = time.perf_counter()
+    leaves, _ = O.ref_perft(O.startpos_cells(), 0, 4, threads=threads)
+    dt = time.perf_counter() - t0
+    out["cpu_baseline"] = {"value": leaves / dt, "unit": "leaf nodes/s", "cores": threads, "kind": "port",
+                           "sample": "refcpu (literal C++ restatement of chess.rs, brute-force over all 4096 "
+                                     f"(from,to) pairs per node) perft(startpos,4) = {leaves} leaves in {dt:.2f}s",
+                           "host_cpus": os.cpu_count()}
+    t0 = time.perf_counter()
+    fl, _, _ = O.fast_perft(O.Pos(), 5, O.REF, threads=threads)
+    dt = time.perf_counter() - t0
+    out["cpu_fast"] = {"value": fl / dt, "unit": "leaf nodes/s", "cores": threads, "kind": "port",
+                       "sample": f"fastcpu mailbox engine perft(startpos,5) = {fl} leaves in {dt:.2f}s"}
+    if not args.no_replay:
+        n = 20_000
+        mv = O.fast_gen_games(0x5EED20241022, 0, n, args.plies, 32, threads=threads)
+        t0 = time.perf_counter()
+        _, _, st = O.ref_replay(mv, threads=threads)
+        dt = time.perf_counter() - t0
+        out["cpu_replay"] = {"value": float(st[0]) / dt, "unit": "validated moves/s", "cores": threads,
+                             "kind": "port", "sample": f"refcpu replay of {n} seeded games x {args.plies} plies "
+                                                       f"({int(st[0])} validated moves) in {dt:.2f}s"}
+    return out
+
+
+def main():
+    args = parse()
+    d = Dist(args.gpus)
+    eng = dchess.Engine(d.local)
+    pos = dchess.startpos()
+    want = REF_STARTPOS.get(args.depth)
+
+    # ---------------------------------------------------------------- perft
+    for _ in range(args.warmup):
+        tot, _, _ = perft_step(eng, d, args, pos)
+        if want is not None and tot != want:
+            raise SystemExit(f"parity failure: perft({args.depth}) = {tot}, expected {want}")
+    eng.reset_stats()
+    eng.set_profiling(True)
+    d.sync()
+    t0 = time.perf_counter()
+    leaves = 0
+    for _ in range(args.steps):
+        tot, _, _ = perft_step(eng, d, args, pos)
+        leaves += tot
+    d.sync()
+    dt = d.max(time.perf_counter() - t0)
+    eng.set_profiling(False)
+    if want is not None and leaves != want * args.steps:
+        raise SystemExit(f"parity failure in timed region: {leaves} != {want} x {args.steps}")
+    c2 = eng.kernel_stats("count2")
+    exp_c = eng.kernel_stats("expand_count")
+    exp_w = eng.kernel_stats("expand_write")
+
+    # --------------------------------------------------------------- replay
+    replay = None
+    if not args.no_replay and args.games > 0:
+        n, plies = args.games, args.plies
+        d_moves = eng.alloc(n * plies * 2)
+        d_bm = eng.alloc(((n + 63) // 64) * plies * 8)
+        d_dg = eng.alloc(n * 8)
+        eng.gen_games_device(d_moves, 0x5EED20241022, d.rank * n, n, plies, 32)  # inputs resident before timing
+        st = eng.replay_device(d_moves, n, plies, d_bm, d_dg)
+        eng.reset_stats()
+        eng.set_profiling(True)
+        d.sync()
+        t0 = time.perf_counter()
+        validated = 0
+        for _ in range(args.replay_steps):
+            st = eng.replay_device(d_moves, n, plies, d_bm, d_dg)
+            validated += st["validated"]
+        d.sync()
+        rdt = d.max(time.perf_counter() - t0)
+        eng.set_profiling(False)
+        rk = eng.kernel_stats("replay")
+        tot_validated = int(d.allreduce_u64(np.array([validated], np.uint64))[0])
+        avg_ms = rk["total_ms"] / max(rk["launches"], 1)
+        replay = {"value": tot_validated / rdt, "unit": "validated moves/s",
+                  "workload": f"{n} seeded games x {plies} ply slots per rank (seed 0x5EED20241022, 1/8 junk moves)",
+                  "scaling": "weak", "ms_per_step": 1e3 * rdt / args.replay_steps,
+                  "kernel_avg_ms": avg_ms, "kernel_moves_per_s": (rk["units"] / max(rk["launches"], 1)) / (avg_ms / 1e3),
+                  "bitmap_checksum": {"accepted": st["accepted"], "digest_xor": st["digest_xor"]}}
+        for b in (d_moves, d_bm, d_dg):
+            b.free()
+
+    if d.rank != 0 or args.profile_only:
+        return
+    avg_ms = c2["total_ms"] / max(c2["launches"], 1)
+    leaves_per_launch = c2["units"] / max(c2["launches"], 1)
+    rate = leaves_per_launch / (avg_ms / 1e3) if avg_ms > 0 else 0.0
+    roof = {"bound": "valu", "unit": "Gops/s (int32 VALU lane-ops)", "kernel": "k_count2",
+            "peak": VALU_PEAK_LANE_OPS / 1e9, "kernel_avg_ms": avg_ms, "kernel_leaves_per_s": rate,
+            "W_lane_ops_per_leaf": W_COUNT2, "traffic": None}
+    if W_COUNT2:
+        roof["achieved"] = rate * W_COUNT2 / 1e9
+        roof["frac"] = roof["achieved"] / roof["peak"]
+    else:
+        roof["achieved"] = None
+        roof["frac"] = None
+    pmc = os.path.join(REPO, "profiles", "pmc_count2.json")
+    if os.path.exists(pmc):
+        p = json.load(open(pmc))
+        roof["traffic"] = p.get("hbm_bytes_per_launch")
+    line = {
+        "metric": METRIC, "value": leaves / dt if dt > 0 else 0.0, "unit": "leaf nodes/s",
+        "n_gpus": d.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (startpos tree; seeded random-legal games for replay)",
+        "config": {"workload": f"perft(startpos, {args.depth}) RULES_REF (bit-exact with core/src/chess.rs), "
+                               f"frontier split at ply {args.split} over ranks", "depth": args.depth,
+                   "rules": "REF", "leaves_per_step": want, "parallelism": f"dp{d.world}"},
+        "roofline": roof,
+        "kernels": {"count2_ms_per_step": c2["total_ms"] / args.steps,
+                    "expand_ms_per_step": (exp_c["total_ms"] + exp_w["total_ms"]) / args.steps},
+    }
+    if replay is not None:
+        line["replay"] = replay
+    if not args.no_cpu and d.world == 1:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        line.update(cpu_baselines(args, threads))
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,774 @@
+// dc_api.hip -- implementation of include/dchess.h (host side of the engine).
+//
+// Owns the per-device context (stream, grow-only device buffers, HIP-event
+// kernel timing) and drives the kernels of dc_kernels.hip.  No rule is ever
+// evaluated on the host: every verdict, count and state update comes from a
+// gfx950 kernel, and every entry point fails with DC_ENODEV when no device
+// is usable -- there is no CPU fallback.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/dchess.h"
+#include "dc_fide.h"
+#include "dc_kernels.h"
+
+using dc::Board;
+using dc::DevPos;
+using dc::u32;
+using dc::u64;
+
+static_assert(sizeof(dc_pos) == sizeof(DevPos), "dc_pos / DevPos layout");
+
+// ------------------------------------------------------------------ buffers
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  size_t cap = 0;
+  hipError_t ensure(size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(n, 64);
+    want = want + want / 4;  // grow with headroom
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+struct PendingEvent {
+  std::string name;
+  hipEvent_t a, b;
+  u64 units;
+};
+
+struct KStat {
+  u64 launches = 0;
+  double ms = 0;
+  u64 units = 0;
+};
+
+struct dc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool profiling = false;
+  std::vector<hipEvent_t> event_pool;
+  std::vector<PendingEvent> pending;
+  std::map<std::string, KStat> stats;
+
+  // perft frontier (ping-pong) and scratch
+  DBuf<Board> nodes[2];
+  DBuf<uint16_t> tags[2];
+  DBuf<uint16_t> meta[2];  // FIDE castle/ep per node
+  DBuf<uint16_t> root_moves;
+  DBuf<u32> counts;
+  DBuf<u64> offsets;
+  DBuf<u64> scan_tmp;
+  DBuf<u64> divide;
+  // batch / replay scratch
+  DBuf<DevPos> pos;
+  DBuf<uint16_t> moves;
+  DBuf<uint8_t> verdicts, info;
+  DBuf<u64> bitmap, digests, stats5;
+
+  ~dc_ctx() {
+    for (auto* b : {&nodes[0], &nodes[1]}) b->release();
+    for (auto* b : {&tags[0], &tags[1], &meta[0], &meta[1], &root_moves, &moves}) b->release();
+    counts.release();
+    offsets.release();
+    scan_tmp.release();
+    divide.release();
+    pos.release();
+    verdicts.release();
+    info.release();
+    bitmap.release();
+    digests.release();
+    stats5.release();
+    for (auto& p : pending) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    for (auto e : event_pool) (void)hipEventDestroy(e);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  hipEvent_t take_event() {
+    if (!event_pool.empty()) {
+      hipEvent_t e = event_pool.back();
+      event_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  // Brackets one launch with events on the context stream when profiling.
+  template <class F>
+  hipError_t timed(const char* name, u64 units, F&& launch) {
+    if (!profiling) return launch();
+    PendingEvent pe{name, take_event(), take_event(), units};
+    (void)hipEventRecord(pe.a, stream);
+    hipError_t e = launch();
+    (void)hipEventRecord(pe.b, stream);
+    pending.push_back(pe);
+    return e;
+  }
+  // After a stream sync: fold pending events into stats.
+  void harvest() {
+    for (auto& p : pending) {
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, p.a, p.b);
+      KStat& s = stats[p.name];
+      s.launches++;
+      s.ms += ms;
+      s.units += p.units;
+      event_pool.push_back(p.a);
+      event_pool.push_back(p.b);
+    }
+    pending.clear();
+  }
+};
+
+#define HIP_TRY(x)                                   \
+  do {                                               \
+    hipError_t _e = (x);                             \
+    if (_e != hipSuccess) return map_hip_error(_e);  \
+  } while (0)
+
+static int map_hip_error(hipError_t e) {
+  if (e == hipErrorOutOfMemory) return DC_ENOMEM;
+  if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return DC_ENODEV;
+  if (e == hipErrorNotSupported) return DC_EUNSUPPORTED;
+  return DC_EHIP;
+}
+
+static int sync_ctx(dc_ctx* c) {
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->harvest();
+  return DC_SUCCESS;
+}
+
+static int enter(dc_ctx* c) {
+  if (!c) return DC_EINVAL;
+  HIP_TRY(hipSetDevice(c->device));
+  return DC_SUCCESS;
+}
+
+#define ENTER(c)                      \
+  do {                                \
+    int _r = enter(c);                \
+    if (_r != DC_SUCCESS) return _r;  \
+  } while (0)
+
+// ================================================================ context
+extern "C" {
+
+int dc_version(void) { return 100; }
+
+const char* dc_strerror(int s) {
+  switch (s) {
+    case DC_SUCCESS: return "success";
+    case DC_EINVAL: return "invalid argument";
+    case DC_EHIP: return "HIP runtime error";
+    case DC_ENOMEM: return "out of memory";
+    case DC_ENODEV: return "no usable gfx950 device";
+    case DC_ERCCL: return "RCCL error";
+    case DC_EUNSUPPORTED: return "unsupported request";
+  }
+  return "unknown status";
+}
+
+const char* dc_verdict_message(uint8_t v) {
+  switch (v) {
+    case DC_V_OK: return "";
+    case DC_V_NO_PIECE: return "No piece at the source location";       // chess.rs:104-106
+    case DC_V_WRONG_TURN: return "It's not this piece's turn to move";  // chess.rs:113-115
+    case DC_V_ILLEGAL: return "Invalid move for the piece";             // chess.rs:119-121
+    case DC_V_OOR: return "Position out of range";
+  }
+  return "Unknown verdict";
+}
+
+int dc_ctx_create(int device, dc_ctx** out) {
+  if (!out) return DC_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return DC_ENODEV;
+  if (device < 0 || device >= n) return DC_ENODEV;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return DC_ENODEV;
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return DC_ENODEV;  // code objects are gfx950-only
+  HIP_TRY(hipSetDevice(device));
+  dc_ctx* c = new dc_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return DC_EHIP;
+  }
+  *out = c;
+  return DC_SUCCESS;
+}
+
+int dc_ctx_destroy(dc_ctx* c) {
+  if (!c) return DC_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  delete c;
+  return DC_SUCCESS;
+}
+
+int dc_ctx_device(const dc_ctx* c) { return c ? c->device : -1; }
+void* dc_ctx_stream(dc_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int dc_ctx_set_profiling(dc_ctx* c, int enable) {
+  if (!c) return DC_EINVAL;
+  c->profiling = enable != 0;
+  return DC_SUCCESS;
+}
+
+int dc_ctx_kernel_stats(dc_ctx* c, const char* kernel, dc_kernel_stats* out) {
+  if (!c || !kernel || !out) return DC_EINVAL;
+  auto it = c->stats.find(kernel);
+  if (it == c->stats.end()) {
+    *out = dc_kernel_stats{0, 0.0, 0};
+  } else {
+    out->launches = it->second.launches;
+    out->total_ms = it->second.ms;
+    out->units = it->second.units;
+  }
+  return DC_SUCCESS;
+}
+
+int dc_ctx_reset_stats(dc_ctx* c) {
+  if (!c) return DC_EINVAL;
+  c->stats.clear();
+  return DC_SUCCESS;
+}
+
+int dc_device_alloc(dc_ctx* c, size_t bytes, void** d_ptr) {
+  ENTER(c);
+  if (!d_ptr) return DC_EINVAL;
+  *d_ptr = nullptr;
+  HIP_TRY(hipMalloc(d_ptr, std::max<size_t>(bytes, 1)));
+  return DC_SUCCESS;
+}
+
+int dc_device_free(dc_ctx* c, void* d_ptr) {
+  ENTER(c);
+  if (d_ptr) HIP_TRY(hipFree(d_ptr));
+  return DC_SUCCESS;
+}
+
+int dc_memcpy_h2d(dc_ctx* c, void* d_dst, const void* src, size_t bytes) {
+  ENTER(c);
+  if (bytes && (!d_dst || !src)) return DC_EINVAL;
+  if (bytes) HIP_TRY(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+  return sync_ctx(c);
+}
+
+int dc_memcpy_d2h(dc_ctx* c, void* dst, const void* d_src, size_t bytes) {
+  ENTER(c);
+  if (bytes && (!dst || !d_src)) return DC_EINVAL;
+  if (bytes) HIP_TRY(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+// ================================================================ adapters
+// Cell kind (P N B R Q K X) -> ABI kind code (P=1 N=2 B=5 R=6 Q=7 K=3 X=4).
+static const int kCellToCode[7] = {1, 2, 5, 6, 7, 3, 4};
+static const int kCodeToCell[8] = {-1, 0, 1, 5, 6, 2, 3, 4};
+
+int dc_startpos(dc_pos* out) {
+  if (!out) return DC_EINVAL;
+  std::memset(out, 0, sizeof *out);
+  out->bb[0] = dc::kStartB0;
+  out->bb[1] = dc::kStartB1;
+  out->bb[2] = dc::kStartB2;
+  out->bb[3] = dc::kStartB3;
+  out->stm = 0;
+  out->castle = 15;
+  out->ep = -1;
+  return DC_SUCCESS;
+}
+
+int dc_pos_from_cells(const int8_t cells[64], uint8_t turn, dc_pos* out) {
+  if (!cells || !out || turn > 1) return DC_EINVAL;  // Color::from_i32 panics otherwise (chess.rs:110)
+  dc_pos p;
+  std::memset(&p, 0, sizeof p);
+  for (int s = 0; s < 64; ++s) {
+    const int8_t c = cells[s];
+    if (c == DC_CELL_EMPTY) continue;
+    if (c < 0 || (c >> 3) > 1 || (c & 7) > 6) return DC_EINVAL;  // colour outside {0,1} is not representable
+    const uint64_t m = 1ull << s;
+    const int code = kCellToCode[c & 7];
+    if (c >> 3) p.bb[0] |= m;
+    if (code & 1) p.bb[1] |= m;
+    if (code & 2) p.bb[2] |= m;
+    if (code & 4) p.bb[3] |= m;
+  }
+  p.stm = turn;
+  p.castle = 0;
+  p.ep = -1;
+  *out = p;
+  return DC_SUCCESS;
+}
+
+int dc_pos_to_cells(const dc_pos* pos, int8_t cells[64], uint8_t* turn) {
+  if (!pos || !cells) return DC_EINVAL;
+  for (int s = 0; s < 64; ++s) {
+    const int code = (int)(((pos->bb[1] >> s) & 1) | (((pos->bb[2] >> s) & 1) << 1) | (((pos->bb[3] >> s) & 1) << 2));
+    if (code == 0) {
+      cells[s] = DC_CELL_EMPTY;
+      continue;
+    }
+    cells[s] = (int8_t)(((pos->bb[0] >> s) & 1) * 8 + kCodeToCell[code]);
+  }
+  if (turn) *turn = pos->stm;
+  return DC_SUCCESS;
+}
+
+int dc_pos_from_fen(const char* fen, dc_pos* out) {
+  if (!fen || !out) return DC_EINVAL;
+  int8_t cells[64];
+  std::memset(cells, DC_CELL_EMPTY, sizeof cells);
+  int x = 7, y = 0;
+  const char* s = fen;
+  for (; *s && *s != ' '; ++s) {
+    if (*s == '/') {
+      if (y != 8 || x == 0) return DC_EINVAL;
+      --x;
+      y = 0;
+      continue;
+    }
+    if (*s >= '1' && *s <= '8') {
+      y += *s - '0';
+      if (y > 8) return DC_EINVAL;
+      continue;
+    }
+    static const char* kinds = "pnbrqk";
+    const char* k = std::strchr(kinds, *s | 0x20);
+    if (!k || y > 7) return DC_EINVAL;
+    cells[8 * x + y] = (int8_t)(((*s >= 'a') ? 8 : 0) + (k - kinds));
+    ++y;
+  }
+  if (x != 0 || y != 8) return DC_EINVAL;
+  while (*s == ' ') ++s;
+  uint8_t stm = 0;
+  if (*s == 'b') stm = 1;
+  else if (*s != 'w') return DC_EINVAL;
+  ++s;
+  while (*s == ' ') ++s;
+  uint8_t castle = 0;
+  for (; *s && *s != ' '; ++s) {
+    switch (*s) {
+      case 'K': castle |= 1; break;
+      case 'Q': castle |= 2; break;
+      case 'k': castle |= 4; break;
+      case 'q': castle |= 8; break;
+      case '-': break;
+      default: return DC_EINVAL;
+    }
+  }
+  while (*s == ' ') ++s;
+  int8_t ep = -1;
+  if (*s >= 'a' && *s <= 'h' && s[1] >= '1' && s[1] <= '8') ep = (int8_t)((s[1] - '1') * 8 + (s[0] - 'a'));
+  int r = dc_pos_from_cells(cells, stm, out);
+  if (r != DC_SUCCESS) return r;
+  out->castle = castle;
+  out->ep = ep;
+  return DC_SUCCESS;
+}
+
+uint16_t dc_move_pack(uint32_t fx, uint32_t fy, uint32_t tx, uint32_t ty) {
+  if (fx >= 8 || fy >= 8 || tx >= 8 || ty >= 8) return (uint16_t)DC_MOVE_OOR;
+  return (uint16_t)((8 * fx + fy) | ((8 * tx + ty) << 6));
+}
+
+// ============================================================== validation
+int dc_validate_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, const uint16_t* moves, uint32_t n,
+                      uint8_t* verdicts) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
+  if (n == 0) return DC_SUCCESS;
+  HIP_TRY(c->pos.ensure(n));
+  HIP_TRY(c->moves.ensure(n));
+  HIP_TRY(c->verdicts.ensure(n));
+  HIP_TRY(hipMemcpyAsync(c->pos.p, pos, sizeof(dc_pos) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->moves.p, moves, sizeof(uint16_t) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c->timed("validate", n, [&] {
+    return rules == DC_RULES_REF ? dc::launch_validate_ref(c->stream, c->pos.p, c->moves.p, n, c->verdicts.p)
+                                 : dc::launch_validate_fide(c->stream, c->pos.p, c->moves.p, n, c->verdicts.p);
+  }));
+  HIP_TRY(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+int dc_apply_batch(dc_ctx* c, uint32_t rules, dc_pos* pos, const uint16_t* moves, uint32_t n, uint8_t* verdicts,
+                   uint8_t* info) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
+  if (n == 0) return DC_SUCCESS;
+  HIP_TRY(c->pos.ensure(n));
+  HIP_TRY(c->moves.ensure(n));
+  HIP_TRY(c->verdicts.ensure(n));
+  HIP_TRY(c->info.ensure(n));
+  HIP_TRY(hipMemcpyAsync(c->pos.p, pos, sizeof(dc_pos) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->moves.p, moves, sizeof(uint16_t) * n, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(c->timed("apply", n, [&] {
+    return rules == DC_RULES_REF
+               ? dc::launch_apply_ref(c->stream, c->pos.p, c->moves.p, n, c->verdicts.p, c->info.p)
+               : dc::launch_apply_fide(c->stream, c->pos.p, c->moves.p, n, c->verdicts.p, c->info.p);
+  }));
+  HIP_TRY(hipMemcpyAsync(pos, c->pos.p, sizeof(dc_pos) * n, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(verdicts, c->verdicts.p, n, hipMemcpyDeviceToHost, c->stream));
+  if (info) HIP_TRY(hipMemcpyAsync(info, c->info.p, n, hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+// ================================================================== replay
+static int replay_impl(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* d_moves, uint32_t n_games,
+                       uint32_t n_plies, u64* d_bitmap, u64* d_digests, dc_replay_stats* stats) {
+  dc_pos s;
+  if (start) s = *start;
+  else dc_startpos(&s);
+  if (s.stm > 1) return DC_EINVAL;
+  HIP_TRY(c->stats5.ensure(5));
+  HIP_TRY(hipMemsetAsync(c->stats5.p, 0, 5 * sizeof(u64), c->stream));
+  const Board b{s.bb[0], s.bb[1], s.bb[2], s.bb[3]};
+  HIP_TRY(c->timed("replay", (u64)n_games * n_plies, [&] {
+    return rules == DC_RULES_REF
+               ? dc::launch_replay_ref(c->stream, b, s.stm, d_moves, n_games, n_plies, d_bitmap, d_digests, c->stats5.p)
+               : dc::launch_replay_fide(c->stream, reinterpret_cast<const DevPos&>(s), d_moves, n_games, n_plies,
+                                        d_bitmap, d_digests, c->stats5.p);
+  }));
+  u64 h[5];
+  HIP_TRY(hipMemcpyAsync(h, c->stats5.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  int r = sync_ctx(c);
+  if (r != DC_SUCCESS) return r;
+  if (stats) {
+    stats->validated = h[0];
+    stats->accepted = h[1];
+    stats->rejected = h[2];
+    stats->digest_sum = h[3];
+    stats->digest_xor = h[4];
+  }
+  // patch the unit count to validated moves (non-sentinel plies)
+  if (c->profiling) {
+    auto& ks = c->stats["replay"];
+    ks.units = ks.units - (u64)n_games * n_plies + h[0];
+  }
+  return DC_SUCCESS;
+}
+
+int dc_replay_device(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* d_moves, uint32_t n_games,
+                     uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests, dc_replay_stats* stats) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n_games && n_plies && !d_moves)) return DC_EINVAL;
+  return replay_impl(c, rules, start, d_moves, n_games, n_plies, reinterpret_cast<u64*>(d_bitmap),
+                     reinterpret_cast<u64*>(d_digests), stats);
+}
+
+int dc_replay(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* moves, uint32_t n_games,
+              uint32_t n_plies, uint64_t* bitmap, uint64_t* digests, dc_replay_stats* stats) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n_games && n_plies && !moves)) return DC_EINVAL;
+  const size_t nm = (size_t)n_games * n_plies;
+  const size_t words = (size_t)((n_games + 63) / 64) * n_plies;
+  HIP_TRY(c->moves.ensure(std::max<size_t>(nm, 1)));
+  if (bitmap) HIP_TRY(c->bitmap.ensure(std::max<size_t>(words, 1)));
+  if (digests) HIP_TRY(c->digests.ensure(std::max<size_t>(n_games, 1)));
+  if (nm) HIP_TRY(hipMemcpyAsync(c->moves.p, moves, nm * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  int r = replay_impl(c, rules, start, c->moves.p, n_games, n_plies, bitmap ? c->bitmap.p : nullptr,
+                      digests ? c->digests.p : nullptr, stats);
+  if (r != DC_SUCCESS) return r;
+  if (bitmap && words)
+    HIP_TRY(hipMemcpyAsync(bitmap, c->bitmap.p, words * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  if (digests && n_games)
+    HIP_TRY(hipMemcpyAsync(digests, c->digests.p, (size_t)n_games * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+int dc_gen_games_device(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games,
+                        uint32_t n_plies, uint32_t noise_per_256, uint16_t* d_out) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n_games && n_plies && !d_out) || noise_per_256 > 256) return DC_EINVAL;
+  if (!n_games || !n_plies) return DC_SUCCESS;
+  HIP_TRY(c->timed("gen_games", (u64)n_games * n_plies, [&] {
+    return rules == DC_RULES_REF
+               ? dc::launch_gen_games_ref(c->stream, seed, first_game, n_games, n_plies, noise_per_256, d_out)
+               : dc::launch_gen_games_fide(c->stream, seed, first_game, n_games, n_plies, noise_per_256, d_out);
+  }));
+  return sync_ctx(c);
+}
+
+int dc_gen_games(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games, uint32_t n_plies,
+                 uint32_t noise_per_256, uint16_t* out) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n_games && n_plies && !out) || noise_per_256 > 256) return DC_EINVAL;
+  const size_t nm = (size_t)n_games * n_plies;
+  if (!nm) return DC_SUCCESS;
+  HIP_TRY(c->moves.ensure(nm));
+  int r = dc_gen_games_device(c, rules, seed, first_game, n_games, n_plies, noise_per_256, c->moves.p);
+  if (r != DC_SUCCESS) return r;
+  HIP_TRY(hipMemcpyAsync(out, c->moves.p, nm * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+}  // extern "C"
+
+// =================================================================== perft
+// Level-synchronous, deterministic frontier: level L+1 = children of level L in
+// (parent, move-class, target) order, so every rank that rebuilds the top levels
+// sees the same frontier and can take a contiguous shard of it.  The last two
+// plies are fused into k_count2 (or the last ply into k_count1).
+namespace {
+
+struct Level {
+  Board* nodes;
+  uint16_t* tags;
+  uint16_t* meta;
+  u64 n;
+};
+
+int expand_level(dc_ctx* c, uint32_t rules, int stm, const Level& in, int dst, bool root, Level* out) {
+  const u32 n = (u32)in.n;
+  HIP_TRY(c->counts.ensure(std::max<u64>(in.n, 1)));
+  HIP_TRY(c->offsets.ensure(std::max<u64>(in.n, 1)));
+  HIP_TRY(c->scan_tmp.ensure(dc::scan_temp_elems(in.n)));
+  HIP_TRY(c->timed("expand_count", in.n, [&] {
+    return rules == DC_RULES_REF ? dc::launch_count_children(c->stream, stm, in.nodes, n, c->counts.p)
+                                 : dc::launch_count_children_fide(c->stream, stm, in.nodes, in.meta, n, c->counts.p);
+  }));
+  HIP_TRY(dc::launch_scan_u32(c->stream, c->counts.p, in.n, c->offsets.p, c->scan_tmp.p));
+  u64 last_off = 0;
+  u32 last_cnt = 0;
+  HIP_TRY(hipMemcpyAsync(&last_off, c->offsets.p + (in.n - 1), sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(&last_cnt, c->counts.p + (in.n - 1), sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+  int r = sync_ctx(c);
+  if (r != DC_SUCCESS) return r;
+  const u64 total = last_off + last_cnt;
+  if (total > 0xFFFFFFFFull) return DC_EUNSUPPORTED;  // frontier > 2^32 nodes: deeper split needed
+  const size_t want = std::max<u64>(total, 1);
+  HIP_TRY(c->nodes[dst].ensure(want));
+  HIP_TRY(c->tags[dst].ensure(want));
+  if (rules == DC_RULES_FIDE) HIP_TRY(c->meta[dst].ensure(want));
+  if (root) HIP_TRY(c->root_moves.ensure(std::max<u64>(total, 1)));
+  HIP_TRY(c->timed("expand_write", total, [&] {
+    return rules == DC_RULES_REF
+               ? dc::launch_expand_write(c->stream, stm, in.nodes, in.tags, n, c->offsets.p, c->nodes[dst].p,
+                                         c->tags[dst].p, root ? c->root_moves.p : nullptr, root ? 1 : 0)
+               : dc::launch_expand_write_fide(c->stream, stm, in.nodes, in.meta, in.tags, n, c->offsets.p,
+                                              c->nodes[dst].p, c->meta[dst].p, c->tags[dst].p,
+                                              root ? c->root_moves.p : nullptr, root ? 1 : 0);
+  }));
+  *out = Level{c->nodes[dst].p, c->tags[dst].p, rules == DC_RULES_FIDE ? c->meta[dst].p : nullptr, total};
+  return DC_SUCCESS;
+}
+
+int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
+               uint32_t n_shards, uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total) {
+  if (!pos || !total || rules > DC_RULES_FIDE || n_shards == 0 || shard >= n_shards || pos->stm > 1) return DC_EINVAL;
+  if (depth > 12) return DC_EUNSUPPORTED;
+  *total = 0;
+  if (n_root) *n_root = 0;
+  if (depth == 0) {
+    *total = (shard == 0) ? 1 : 0;
+    return DC_SUCCESS;
+  }
+  // level 0: the root
+  HIP_TRY(c->nodes[0].ensure(1));
+  HIP_TRY(c->tags[0].ensure(1));
+  HIP_TRY(c->meta[0].ensure(1));
+  const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
+  const uint16_t zero = 0;
+  const uint16_t rmeta = dc::pack_meta(pos->castle, pos->ep);
+  HIP_TRY(hipMemcpyAsync(c->nodes[0].p, &rb, sizeof rb, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->tags[0].p, &zero, sizeof zero, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->meta[0].p, &rmeta, sizeof rmeta, hipMemcpyHostToDevice, c->stream));
+  Level cur{c->nodes[0].p, c->tags[0].p, rules == DC_RULES_FIDE ? c->meta[0].p : nullptr, 1};
+  Level nxt;
+  int r = expand_level(c, rules, pos->stm, cur, 1, true, &nxt);
+  if (r != DC_SUCCESS) return r;
+  cur = nxt;
+  const u32 nr = (u32)cur.n;
+  if (nr > 256) return DC_EUNSUPPORTED;
+  if (n_root) *n_root = nr;
+  std::vector<uint16_t> rm(nr);
+  if (nr) HIP_TRY(hipMemcpyAsync(rm.data(), c->root_moves.p, nr * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c->divide.ensure(256));
+  HIP_TRY(hipMemsetAsync(c->divide.p, 0, 256 * sizeof(u64), c->stream));
+  r = sync_ctx(c);
+  if (r != DC_SUCCESS) return r;
+  if (root_moves) std::copy(rm.begin(), rm.end(), root_moves);
+  std::vector<u64> div(nr, 0);
+  if (depth == 1) {
+    if (shard == 0)
+      for (u32 i = 0; i < nr; ++i) div[i] = 1;
+  } else {
+    const u32 final_level = depth >= 3 ? depth - 2 : 1;
+    const u32 split = std::max<u32>(1, std::min(split_depth, final_level));
+    u32 level = 1;
+    int buf = 1;
+    auto apply_shard = [&]() {
+      if (n_shards == 1) return;
+      const u64 lo = cur.n * shard / n_shards, hi = cur.n * (shard + 1) / n_shards;
+      cur.nodes += lo;
+      cur.tags += lo;
+      if (cur.meta) cur.meta += lo;
+      cur.n = hi - lo;
+    };
+    while (level < final_level) {
+      if (level == split) apply_shard();
+      if (cur.n == 0) break;
+      r = expand_level(c, rules, pos->stm ^ (level & 1), cur, buf ^ 1, false, &nxt);
+      if (r != DC_SUCCESS) return r;
+      cur = nxt;
+      buf ^= 1;
+      ++level;
+    }
+    if (level == split && level == final_level) apply_shard();
+    const int stm = pos->stm ^ (level & 1);
+    if (cur.n) {
+      if (depth >= 3) {
+        // leaves = grandchildren of the final level
+        HIP_TRY(c->timed("count2", 0, [&] {
+          return rules == DC_RULES_REF
+                     ? dc::launch_count2(c->stream, stm, cur.nodes, cur.tags, (u32)cur.n, c->divide.p, 0)
+                     : dc::launch_count2_fide(c->stream, stm, cur.nodes, cur.meta, cur.tags, (u32)cur.n, c->divide.p, 0);
+        }));
+      } else {
+        HIP_TRY(c->timed("count1", 0, [&] {
+          return rules == DC_RULES_REF
+                     ? dc::launch_count1(c->stream, stm, cur.nodes, cur.tags, (u32)cur.n, c->divide.p)
+                     : dc::launch_count1_fide(c->stream, stm, cur.nodes, cur.meta, cur.tags, (u32)cur.n, c->divide.p);
+        }));
+      }
+    }
+    HIP_TRY(hipMemcpyAsync(div.data(), c->divide.p, nr * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+    r = sync_ctx(c);
+    if (r != DC_SUCCESS) return r;
+    u64 leaves = 0;
+    for (u32 i = 0; i < nr; ++i) leaves += div[i];
+    if (c->profiling) {
+      auto it = c->stats.find(depth >= 3 ? "count2" : "count1");
+      if (it != c->stats.end()) it->second.units += leaves;
+    }
+  }
+  u64 t = 0;
+  for (u32 i = 0; i < nr; ++i) {
+    t += div[i];
+    if (divide) divide[i] = div[i];
+  }
+  *total = t;
+  return DC_SUCCESS;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dc_perft(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint64_t* divide, uint16_t* root_moves,
+             uint32_t* n_root, uint64_t* total) {
+  ENTER(c);
+  return perft_impl(c, rules, pos, depth, 1, 0, 1, divide, root_moves, n_root, total);
+}
+
+int dc_perft_shard(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
+                   uint32_t n_shards, uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total) {
+  ENTER(c);
+  return perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, divide, root_moves, n_root, total);
+}
+
+// One process, several GPUs: a host thread per device computes its shard of
+// the frontier, then one grouped ncclAllReduce(ncclUint64, ncclSum) over the
+// per-device divide[] vectors combines them over xGMI.
+int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_pos* pos, uint32_t depth,
+                   uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total) {
+  if (!devices || n_devices <= 0 || !pos || !total) return DC_EINVAL;
+  std::vector<dc_ctx*> ctx(n_devices, nullptr);
+  for (int i = 0; i < n_devices; ++i) {
+    int r = dc_ctx_create(devices[i], &ctx[i]);
+    if (r != DC_SUCCESS) {
+      for (auto* x : ctx)
+        if (x) dc_ctx_destroy(x);
+      return r;
+    }
+  }
+  const u32 split = depth >= 5 ? 3 : (depth >= 3 ? depth - 2 : 1);
+  std::vector<int> rc(n_devices, DC_SUCCESS);
+  std::vector<uint32_t> nroot(n_devices, 0);
+  std::vector<uint16_t> rm(256);
+  std::vector<std::thread> th;
+  for (int i = 0; i < n_devices; ++i)
+    th.emplace_back([&, i] {
+      uint64_t tot = 0;
+      rc[i] = dc_perft_shard(ctx[i], rules, pos, depth, split, (u32)i, (u32)n_devices, nullptr,
+                             i == 0 ? rm.data() : nullptr, &nroot[i], &tot);
+    });
+  for (auto& t : th) t.join();
+  int result = DC_SUCCESS;
+  for (int r : rc)
+    if (r != DC_SUCCESS) result = r;
+  std::vector<u64> div(256, 0);
+  if (result == DC_SUCCESS && depth > 0) {
+    std::vector<ncclComm_t> comms(n_devices);
+    if (ncclCommInitAll(comms.data(), n_devices, devices) != ncclSuccess) {
+      result = DC_ERCCL;
+    } else {
+      ncclGroupStart();
+      for (int i = 0; i < n_devices; ++i) {
+        (void)hipSetDevice(devices[i]);
+        ncclAllReduce(ctx[i]->divide.p, ctx[i]->divide.p, nroot[0], ncclUint64, ncclSum, comms[i], ctx[i]->stream);
+      }
+      if (ncclGroupEnd() != ncclSuccess) result = DC_ERCCL;
+      for (int i = 0; i < n_devices; ++i) {
+        (void)hipSetDevice(devices[i]);
+        if (hipStreamSynchronize(ctx[i]->stream) != hipSuccess) result = DC_EHIP;
+      }
+      if (result == DC_SUCCESS) {
+        (void)hipSetDevice(devices[0]);
+        if (hipMemcpy(div.data(), ctx[0]->divide.p, nroot[0] * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess)
+          result = DC_EHIP;
+      }
+      for (auto& cm : comms) ncclCommDestroy(cm);
+    }
+  }
+  if (result == DC_SUCCESS) {
+    u64 t = 0;
+    if (depth == 0) t = 1;
+    for (u32 i = 0; i < nroot[0]; ++i) {
+      t += div[i];
+      if (divide) divide[i] = div[i];
+    }
+    if (depth == 1) {
+      t = nroot[0];
+      if (divide)
+        for (u32 i = 0; i < nroot[0]; ++i) divide[i] = 1;
+    }
+    if (root_moves) std::copy(rm.begin(), rm.begin() + nroot[0], root_moves);
+    if (n_root) *n_root = nroot[0];
+    *total = t;
+  }
+  for (auto* x : ctx) dc_ctx_destroy(x);
+  return result;
+}
+
+}  // extern "C"

@@ -1,0 +1,157 @@
+// dc_bits.h -- gfx950 device primitives on 64-bit boards (one lane = one position).
+//
+// Square s = 8*x + y (x = row, 0 = White's back rank; y = column), as in
+// core/src/chess.rs:127-131 / :394-431.  All arithmetic is integer VALU work:
+// a 64-bit logic op is two v_*_b32, a 64-bit shift is one v_lshlrev_b64 /
+// v_lshrrev_b64, a popcount is two v_bcnt_u32_b32 (the second accumulates).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dc {
+
+typedef unsigned long long u64;
+typedef uint32_t u32;
+
+constexpr u64 kFileA = 0x0101010101010101ull;  // y == 0
+constexpr u64 kFileB = kFileA << 1;
+constexpr u64 kFileG = kFileA << 6;
+constexpr u64 kFileH = kFileA << 7;  // y == 7
+constexpr u64 kNotA = ~kFileA;
+constexpr u64 kNotH = ~kFileH;
+constexpr u64 kNotAB = ~(kFileA | kFileB);
+constexpr u64 kNotGH = ~(kFileG | kFileH);
+constexpr u64 kRow(int x) { return 0xFFull << (8 * x); }
+constexpr u64 kAll = ~0ull;
+constexpr u64 kDiagMain = 0x8040201008040201ull;  // a1..h8 (x - y == 0)
+constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
+
+// Generalised shift: S > 0 toward higher squares.
+template <int S>
+__device__ __forceinline__ u64 sh(u64 x) {
+  if constexpr (S >= 0) return x << S;
+  else return x >> (-S);
+}
+
+__device__ __forceinline__ u32 pc(u64 x) { return (u32)__popcll(x); }
+__device__ __forceinline__ int lsb(u64 x) { return __ffsll((long long)x) - 1; }
+__device__ __forceinline__ int msb(u64 x) { return 63 - __clzll((long long)x); }
+
+// Kogge-Stone occluded fill + one step: the attack set of all sliders in
+// `gen` toward direction S (wrap guard M applied after every step).  In one
+// direction each target has exactly one source (the first piece behind it),
+// so popcount(attacks & ~own) counts moves with multiplicity.
+template <int S, u64 M>
+__device__ __forceinline__ u64 ray_attacks(u64 gen, u64 empty) {
+  u64 pro = empty & M;
+  gen |= pro & sh<S>(gen);
+  pro &= sh<S>(pro);
+  gen |= pro & sh<2 * S>(gen);
+  pro &= sh<2 * S>(pro);
+  gen |= pro & sh<4 * S>(gen);
+  return sh<S>(gen) & M;
+}
+
+// The squares of the line through t in direction class D, strictly on the
+// side the source of a slider move toward direction D lies (i.e. "behind" t).
+// D: 0 N(+8) 1 S(-8) 2 E(+1) 3 W(-1) 4 NE(+9) 5 SW(-9) 6 NW(+7) 7 SE(-7).
+template <int D>
+__device__ __forceinline__ u64 line_behind(int t) {
+  const int x = t >> 3, y = t & 7;
+  u64 line;
+  if constexpr (D == 0 || D == 1) line = kFileA << y;
+  else if constexpr (D == 2 || D == 3) line = 0xFFull << (8 * x);
+  else if constexpr (D == 4 || D == 5) {
+    const int d = x - y;
+    line = d >= 0 ? (kDiagMain << (8 * d)) : (kDiagMain >> (-8 * d));
+  } else {
+    const int a = x + y - 7;
+    line = a >= 0 ? (kDiagAnti << (8 * a)) : (kDiagAnti >> (-8 * a));
+  }
+  const u64 bit = 1ull << t;
+  // even D: positive shift, source below t; odd D: source above t
+  if constexpr ((D & 1) == 0) return line & (bit - 1);
+  else return line & ~(bit | (bit - 1));
+}
+
+// Source square of a slider move toward D that lands on t: the nearest
+// occupied square behind t.
+template <int D>
+__device__ __forceinline__ int slider_source(u64 occ, int t) {
+  const u64 c = occ & line_behind<D>(t);
+  if constexpr ((D & 1) == 0) return msb(c);
+  else return lsb(c);
+}
+
+// Squares strictly between two squares that share a rank, file or diagonal;
+// 0 otherwise (table-free obstruction difference, LERF mapping).
+__device__ __forceinline__ u64 between(int s1, int s2) {
+  const u64 m1 = ~0ull;
+  const u64 a2a7 = 0x0001010101010100ull;
+  const u64 b2g7 = 0x0040201008040200ull;
+  const u64 h1b7 = 0x0002040810204080ull;
+  const u64 btwn = (m1 << s1) ^ (m1 << s2);
+  const u64 file = (u64)((s2 & 7) - (s1 & 7));
+  const u64 rank = (u64)(((s2 | 7) - s1) >> 3);
+  u64 line = ((file & 7) - 1) & a2a7;
+  line += 2 * (((rank & 7) - 1) >> 58);
+  line += (((rank - file) & 15) - 1) & b2g7;
+  line += (((rank + file) & 15) - 1) & h1b7;
+  line *= btwn & (0 - btwn);
+  return line & btwn;
+}
+
+__device__ __forceinline__ u64 fmix64(u64 k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+__device__ __forceinline__ u64 splitmix_next(u64& s) {
+  u64 z = (s += 0x9E3779B97F4A7C15ull);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// k-th (0-based) set bit of x; x must have more than k bits set.
+__device__ __forceinline__ int select_bit(u64 x, u32 k) {
+  const u32 lo = (u32)x;
+  const u32 nlo = (u32)__popc(lo);
+  int base = 0;
+  u32 w = lo;
+  if (k >= nlo) {
+    k -= nlo;
+    w = (u32)(x >> 32);
+    base = 32;
+  }
+  for (u32 i = 0; i < k; ++i) w &= w - 1;
+  return base + __ffs(w) - 1;
+}
+
+// ---------------------------------------------------------------- wave ops
+__device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
+
+__device__ __forceinline__ u32 lane_id() { return __lane_id(); }
+
+// Inclusive prefix sum over the 64 lanes of a wave.
+__device__ __forceinline__ u32 wave_incl_scan(u32 v) {
+  const int lane = (int)lane_id();
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const u32 n = __shfl_up(v, o, 64);
+    if (lane >= o) v += n;
+  }
+  return v;
+}
+
+__device__ __forceinline__ u64 wave_sum64(u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace dc

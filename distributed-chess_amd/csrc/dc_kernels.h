@@ -1,0 +1,57 @@
+// dc_kernels.h -- launch wrappers of dc_kernels.hip (host side of the engine).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace dc {
+
+typedef unsigned long long u64;
+typedef uint32_t u32;
+
+// One position: quad-bitboard of include/dchess.h (b0 black, b1..b3 kind bits).
+struct Board {
+  u64 b0, b1, b2, b3;
+};
+
+// Device image of dc_pos (include/dchess.h), 40 bytes.
+struct DevPos {
+  u64 bb[4];
+  uint8_t stm, castle;
+  int8_t ep;
+  uint8_t r0;
+  uint32_t r1;
+};
+static_assert(sizeof(DevPos) == 40, "dc_pos layout");
+
+// Startpos quad-bitboard (chess.rs:383-434): b0 black, b1..b3 kind bits.
+constexpr u64 kStartB0 = 0xFFFF000000000000ull;
+constexpr u64 kStartB1 = 0x3CFF00000000FF3Cull;
+constexpr u64 kStartB2 = 0xDB000000000000DBull;
+constexpr u64 kStartB3 = 0xAD000000000000ADull;
+
+template <class B>
+__host__ __device__ inline void startpos_board(B& b) {
+  b.b0 = kStartB0;
+  b.b1 = kStartB1;
+  b.b2 = kStartB2;
+  b.b3 = kStartB3;
+}
+
+hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out);
+hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
+                            uint8_t* info);
+hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
+                             u32 n_plies, u64* bitmap, u64* digests, u64* stats);
+hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
+                                uint16_t* out);
+hipError_t launch_count_children(hipStream_t st, int stm, const Board* nodes, u32 n, u32* counts);
+hipError_t launch_expand_write(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n,
+                               const u64* offsets, Board* out, uint16_t* out_tags, uint16_t* out_moves,
+                               int root_level);
+hipError_t launch_count1(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide);
+hipError_t launch_count2(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide,
+                         u32 max_blocks);
+size_t scan_temp_elems(u64 n);
+hipError_t launch_scan_u32(hipStream_t st, const u32* in, u64 n, u64* out, u64* temp);
+
+}  // namespace dc

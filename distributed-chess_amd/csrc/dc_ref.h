@@ -1,0 +1,260 @@
+// dc_ref.h -- the reference's move rules (RULES_REF) as set-wise bitboard code.
+//
+// Semantics restated from /root/reference/core/src/chess.rs:
+//   validate_move  chess.rs:82-125   (OOR first, then NO_PIECE, WRONG_TURN, ILLEGAL)
+//   can_move_to    chess.rs:199-212  (dispatch on kind; unknown kind never moves)
+//   pawn           chess.rs:214-254  (push, double from row 1/6, diagonal onto enemy;
+//                                     no en passant, no promotion)
+//   rook/bishop    chess.rs:256-335  (aligned, path empty, target empty-or-enemy)
+//   knight/king    chess.rs:289-300, :350-360 (no castling, no check test)
+//   apply_move     chess.rs:43-80    (to <- from, from <- empty, turn flips)
+// "Enemy" is any piece whose colour differs from the mover's (chess.rs:444).
+//
+// Board: quad-bitboard of include/dchess.h -- b0 = black, b1..b3 = kind bits,
+// kind codes P=1 N=2 K=3 OTHER=4 B=5 R=6 Q=7.
+#pragma once
+#include <type_traits>
+
+#include "dc_bits.h"
+#include "dc_kernels.h"
+
+namespace dc {
+
+enum : u32 { V_OK = 0, V_NO_PIECE = 1, V_WRONG_TURN = 2, V_ILLEGAL = 3, V_OOR = 4 };
+enum : u32 { KC_P = 1, KC_N = 2, KC_K = 3, KC_X = 4, KC_B = 5, KC_R = 6, KC_Q = 7 };
+
+__device__ __forceinline__ u64 occupied(const Board& b) { return b.b1 | b.b2 | b.b3; }
+__device__ __forceinline__ u32 nibble(const Board& b, int s) {
+  return (u32)(((b.b0 >> s) & 1) | (((b.b1 >> s) & 1) << 1) | (((b.b2 >> s) & 1) << 2) |
+               (((b.b3 >> s) & 1) << 3));
+}
+
+// Own pieces split into the move classes the generator iterates.
+struct Sides {
+  u64 occ, own, enemy, empty, notown;
+  u64 P, N, K, D, O;  // pawns, knights, kings, diagonal sliders (B,Q), orthogonal (R,Q)
+};
+
+template <int STM>
+__device__ __forceinline__ Sides sides(const Board& b) {
+  Sides s;
+  s.occ = occupied(b);
+  s.own = STM ? b.b0 : (s.occ & ~b.b0);
+  s.enemy = s.occ ^ s.own;
+  s.empty = ~s.occ;
+  s.notown = ~s.own;
+  const u64 lo = b.b1, mid = b.b2, hi = b.b3;
+  s.P = s.own & lo & ~(mid | hi);
+  s.N = s.own & mid & ~(lo | hi);
+  s.K = s.own & lo & mid & ~hi;
+  s.D = s.own & hi & lo;
+  s.O = s.own & hi & mid;
+  return s;
+}
+
+// Pawn target sets (per direction class; sources = target - delta).
+template <int STM>
+struct PawnDir {
+  static constexpr int F = STM ? -8 : 8;      // forward
+  static constexpr int CW = STM ? -9 : 7;     // capture toward column y-1
+  static constexpr int CE = STM ? -7 : 9;     // capture toward column y+1
+  static constexpr u64 ROW_AFTER1 = STM ? kRow(5) : kRow(2);  // single pushes from the start row land here
+};
+
+// Bulk count of REF moves for the side to move: the number of (from,to) pairs
+// validate_move accepts.  Every term is a popcount over one direction class, so
+// multiplicity is exact (two knights reaching one square count twice).
+template <int STM>
+__device__ __forceinline__ u32 ref_count(const Board& b) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 push1 = sh<PD::F>(s.P) & s.empty;
+  const u64 push2 = sh<PD::F>(push1 & PD::ROW_AFTER1) & s.empty;
+  u32 c = pc(push1) + pc(push2);
+  c += pc(sh<PD::CW>(s.P & kNotA) & s.enemy);
+  c += pc(sh<PD::CE>(s.P & kNotH) & s.enemy);
+  const u64 no = s.notown;
+  const u64 n = s.N;
+  c += pc(sh<17>(n & kNotH) & no) + pc(sh<15>(n & kNotA) & no);
+  c += pc(sh<10>(n & kNotGH) & no) + pc(sh<6>(n & kNotAB) & no);
+  c += pc(sh<-6>(n & kNotGH) & no) + pc(sh<-10>(n & kNotAB) & no);
+  c += pc(sh<-15>(n & kNotH) & no) + pc(sh<-17>(n & kNotA) & no);
+  const u64 k = s.K;
+  c += pc(sh<8>(k) & no) + pc(sh<-8>(k) & no);
+  c += pc(sh<1>(k & kNotH) & no) + pc(sh<-1>(k & kNotA) & no);
+  c += pc(sh<9>(k & kNotH) & no) + pc(sh<7>(k & kNotA) & no);
+  c += pc(sh<-7>(k & kNotH) & no) + pc(sh<-9>(k & kNotA) & no);
+  const u64 e = s.empty;
+  c += pc(ray_attacks<8, kAll>(s.O, e) & no) + pc(ray_attacks<-8, kAll>(s.O, e) & no);
+  c += pc(ray_attacks<1, kNotA>(s.O, e) & no) + pc(ray_attacks<-1, kNotH>(s.O, e) & no);
+  c += pc(ray_attacks<9, kNotA>(s.D, e) & no) + pc(ray_attacks<-9, kNotH>(s.D, e) & no);
+  c += pc(ray_attacks<7, kNotH>(s.D, e) & no) + pc(ray_attacks<-7, kNotA>(s.D, e) & no);
+  return c;
+}
+
+// Runtime side-to-move version.
+__device__ __forceinline__ u32 ref_count_rt(const Board& b, u32 stm) {
+  return stm ? ref_count<1>(b) : ref_count<0>(b);
+}
+
+// apply_move's board effect (chess.rs:72-77): the mover's nibble goes to t
+// (overwriting any captured piece, kings included), f becomes empty.
+__device__ __forceinline__ void ref_make(Board& b, int f, int t) {
+  const u64 keep = ~((1ull << f) | (1ull << t));
+  b.b0 = (b.b0 & keep) | (((b.b0 >> f) & 1) << t);
+  b.b1 = (b.b1 & keep) | (((b.b1 >> f) & 1) << t);
+  b.b2 = (b.b2 & keep) | (((b.b2 >> f) & 1) << t);
+  b.b3 = (b.b3 & keep) | (((b.b3 >> f) & 1) << t);
+}
+
+// validate_move on one (position, move word).  Verdict order chess.rs:82-125.
+__device__ __forceinline__ u32 ref_verdict(const Board& b, u32 stm, u32 m) {
+  if (m & 0x8000u) return V_OOR;
+  const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
+  const u32 nib = nibble(b, f);
+  const u32 kind = nib >> 1;
+  if (kind == 0) return V_NO_PIECE;
+  if ((nib & 1) != stm) return V_WRONG_TURN;
+  const u64 occ = occupied(b);
+  const u64 own = stm ? b.b0 : (occ & ~b.b0);
+  const u64 tm = 1ull << t;
+  const int dx = (t >> 3) - (f >> 3), dy = (t & 7) - (f & 7);
+  const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
+  bool ok;
+  switch (kind) {
+    case KC_P: {
+      const int dir = stm ? -1 : 1;
+      const bool t_empty = (occ & tm) == 0;
+      const bool push = dy == 0 && dx == dir && t_empty;
+      const bool dbl = dy == 0 && dx == 2 * dir && (f >> 3) == (stm ? 6 : 1) && t_empty &&
+                       ((occ >> (f + 8 * dir)) & 1) == 0;
+      const bool cap = ay == 1 && dx == dir && (occ & ~own & tm) != 0;
+      ok = push || dbl || cap;
+      break;
+    }
+    case KC_N: ok = (ax == 1 && ay == 2) || (ax == 2 && ay == 1); break;
+    case KC_K: ok = ax <= 1 && ay <= 1; break;
+    case KC_B: ok = ax == ay && (between(f, t) & occ) == 0; break;
+    case KC_R: ok = (dx == 0 || dy == 0) && (between(f, t) & occ) == 0; break;
+    case KC_Q: ok = (ax == ay || dx == 0 || dy == 0) && (between(f, t) & occ) == 0; break;
+    default: ok = false;  // unknown kind string: can_move_to returns false (chess.rs:210)
+  }
+  // target must be empty or enemy for every kind (pawn rules already imply it)
+  ok = ok && (own & tm) == 0;
+  return ok ? V_OK : V_ILLEGAL;
+}
+
+__device__ __forceinline__ u64 board_digest(const Board& b, u32 stm) {
+  u64 h = 0x6A09E667F3BCC909ull ^ (u64)(stm & 1);
+  h = fmix64(h ^ b.b3);
+  h = fmix64(h ^ b.b2);
+  h = fmix64(h ^ b.b1);
+  h = fmix64(h ^ b.b0);
+  return h;
+}
+
+// Target set of one REF piece (for the canonical-order generator).
+__device__ __forceinline__ u64 ref_piece_targets(const Board& b, int f, u32 stm, u32 kind) {
+  const u64 occ = occupied(b);
+  const u64 own = stm ? b.b0 : (occ & ~b.b0);
+  const u64 enemy = occ & ~own, empty = ~occ, no = ~own;
+  const u64 bit = 1ull << f;
+  switch (kind) {
+    case KC_P: {
+      u64 p1, p2, c;
+      if (stm == 0) {
+        p1 = (bit << 8) & empty;
+        p2 = ((p1 & kRow(2)) << 8) & empty;
+        c = (((bit & kNotA) << 7) | ((bit & kNotH) << 9)) & enemy;
+      } else {
+        p1 = (bit >> 8) & empty;
+        p2 = ((p1 & kRow(5)) >> 8) & empty;
+        c = (((bit & kNotA) >> 9) | ((bit & kNotH) >> 7)) & enemy;
+      }
+      return p1 | p2 | c;
+    }
+    case KC_N:
+      return (sh<17>(bit & kNotH) | sh<15>(bit & kNotA) | sh<10>(bit & kNotGH) | sh<6>(bit & kNotAB) |
+              sh<-6>(bit & kNotGH) | sh<-10>(bit & kNotAB) | sh<-15>(bit & kNotH) | sh<-17>(bit & kNotA)) &
+             no;
+    case KC_K:
+      return (sh<8>(bit) | sh<-8>(bit) | sh<1>(bit & kNotH) | sh<-1>(bit & kNotA) | sh<9>(bit & kNotH) |
+              sh<7>(bit & kNotA) | sh<-7>(bit & kNotH) | sh<-9>(bit & kNotA)) &
+             no;
+    case KC_B:
+    case KC_R:
+    case KC_Q: {
+      u64 a = 0;
+      if (kind != KC_B)
+        a |= ray_attacks<8, kAll>(bit, empty) | ray_attacks<-8, kAll>(bit, empty) |
+             ray_attacks<1, kNotA>(bit, empty) | ray_attacks<-1, kNotH>(bit, empty);
+      if (kind != KC_R)
+        a |= ray_attacks<9, kNotA>(bit, empty) | ray_attacks<-9, kNotH>(bit, empty) |
+             ray_attacks<7, kNotH>(bit, empty) | ray_attacks<-7, kNotA>(bit, empty);
+      return a & no;
+    }
+    default: return 0;
+  }
+}
+
+// ------------------------------------------------------------------------
+// Move classes for enumeration.  Class c's target set and source rule:
+//   0 push1, 1 push2, 2 capture toward y-1, 3 capture toward y+1,
+//   4..11 knight offsets, 12..19 king offsets, 20..23 orthogonal rays N,S,E,W,
+//   24..27 diagonal rays NE,SW,NW,SE.
+// The visitor gets (from, to) for every move; order is class-major, target
+// ascending within a class (deterministic).
+template <int STM, class Visit>
+__device__ __forceinline__ void ref_for_each_move(const Board& b, Visit&& visit) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 no = s.notown, e = s.empty;
+  auto leap = [&](u64 targets, int delta) {
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(t - delta, t);
+    }
+  };
+  const u64 push1 = sh<PD::F>(s.P) & e;
+  leap(push1, PD::F);
+  leap(sh<PD::F>(push1 & PD::ROW_AFTER1) & e, 2 * PD::F);
+  leap(sh<PD::CW>(s.P & kNotA) & s.enemy, PD::CW);
+  leap(sh<PD::CE>(s.P & kNotH) & s.enemy, PD::CE);
+  const u64 n = s.N;
+  leap(sh<17>(n & kNotH) & no, 17);
+  leap(sh<15>(n & kNotA) & no, 15);
+  leap(sh<10>(n & kNotGH) & no, 10);
+  leap(sh<6>(n & kNotAB) & no, 6);
+  leap(sh<-6>(n & kNotGH) & no, -6);
+  leap(sh<-10>(n & kNotAB) & no, -10);
+  leap(sh<-15>(n & kNotH) & no, -15);
+  leap(sh<-17>(n & kNotA) & no, -17);
+  const u64 k = s.K;
+  leap(sh<8>(k) & no, 8);
+  leap(sh<-8>(k) & no, -8);
+  leap(sh<1>(k & kNotH) & no, 1);
+  leap(sh<-1>(k & kNotA) & no, -1);
+  leap(sh<9>(k & kNotH) & no, 9);
+  leap(sh<7>(k & kNotA) & no, 7);
+  leap(sh<-7>(k & kNotH) & no, -7);
+  leap(sh<-9>(k & kNotA) & no, -9);
+  auto slide = [&](u64 targets, auto dtag) {
+    constexpr int D = decltype(dtag)::value;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(slider_source<D>(s.occ, t), t);
+    }
+  };
+  slide(ray_attacks<8, kAll>(s.O, e) & no, std::integral_constant<int, 0>{});
+  slide(ray_attacks<-8, kAll>(s.O, e) & no, std::integral_constant<int, 1>{});
+  slide(ray_attacks<1, kNotA>(s.O, e) & no, std::integral_constant<int, 2>{});
+  slide(ray_attacks<-1, kNotH>(s.O, e) & no, std::integral_constant<int, 3>{});
+  slide(ray_attacks<9, kNotA>(s.D, e) & no, std::integral_constant<int, 4>{});
+  slide(ray_attacks<-9, kNotH>(s.D, e) & no, std::integral_constant<int, 5>{});
+  slide(ray_attacks<7, kNotH>(s.D, e) & no, std::integral_constant<int, 6>{});
+  slide(ray_attacks<-7, kNotA>(s.D, e) & no, std::integral_constant<int, 7>{});
+}
+
+}  // namespace dc

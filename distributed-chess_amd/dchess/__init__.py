@@ -1,0 +1,409 @@
+"""dchess -- Python binding of libdchess.so (include/dchess.h) via ctypes.
+
+This is plumbing for tests and bench.py: every call goes through the C ABI to
+the gfx950 kernels.  There is no CPU fallback: if the shared library is missing
+or no gfx950 device is present, the calls raise.
+
+It also mirrors the reference's Rust call surface (core/src/chess.rs) in
+`GameState` / `Position` / `AppError`, so parity tests read like the
+reference's own unit tests (core/src/chess.rs:499-557).
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libdchess.so")
+
+SUCCESS, EINVAL, EHIP, ENOMEM, ENODEV, ERCCL, EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
+V_OK, V_NO_PIECE, V_WRONG_TURN, V_ILLEGAL, V_OOR = 0, 1, 2, 3, 4
+RULES_REF, RULES_FIDE = 0, 1
+MOVE_OOR, MOVE_NONE = 0x8000, 0xFFFF
+CELL_EMPTY = -1
+KINDS = "PNBRQKX"  # cell kind order of the ABI (X = unknown kind string)
+
+POS_DTYPE = np.dtype([("bb", "<u8", (4,)), ("stm", "u1"), ("castle", "u1"), ("ep", "i1"), ("r0", "u1"),
+                      ("r1", "<u4")])
+assert POS_DTYPE.itemsize == 40
+
+
+class DChessError(RuntimeError):
+    def __init__(self, status, what=""):
+        self.status = status
+        super().__init__(f"{what}: {lib().dc_strerror(status).decode()} ({status})")
+
+
+class _Stats(C.Structure):
+    _fields_ = [("validated", C.c_uint64), ("accepted", C.c_uint64), ("rejected", C.c_uint64),
+                ("digest_sum", C.c_uint64), ("digest_xor", C.c_uint64)]
+
+
+class _KStats(C.Structure):
+    _fields_ = [("launches", C.c_uint64), ("total_ms", C.c_double), ("units", C.c_uint64)]
+
+
+_LIB = None
+_vp = C.c_void_p
+
+
+def lib():
+    """Loads libdchess.so (built by __graft_entry__.build()); raises if absent."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"libdchess.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    sig = {
+        "dc_ctx_create": (C.c_int, [C.c_int, C.POINTER(_vp)]),
+        "dc_ctx_destroy": (C.c_int, [_vp]),
+        "dc_ctx_device": (C.c_int, [_vp]),
+        "dc_ctx_stream": (_vp, [_vp]),
+        "dc_strerror": (C.c_char_p, [C.c_int]),
+        "dc_verdict_message": (C.c_char_p, [C.c_uint8]),
+        "dc_version": (C.c_int, []),
+        "dc_ctx_set_profiling": (C.c_int, [_vp, C.c_int]),
+        "dc_ctx_kernel_stats": (C.c_int, [_vp, C.c_char_p, C.POINTER(_KStats)]),
+        "dc_ctx_reset_stats": (C.c_int, [_vp]),
+        "dc_device_alloc": (C.c_int, [_vp, C.c_size_t, C.POINTER(_vp)]),
+        "dc_device_free": (C.c_int, [_vp, _vp]),
+        "dc_memcpy_h2d": (C.c_int, [_vp, _vp, _vp, C.c_size_t]),
+        "dc_memcpy_d2h": (C.c_int, [_vp, _vp, _vp, C.c_size_t]),
+        "dc_startpos": (C.c_int, [_vp]),
+        "dc_pos_from_cells": (C.c_int, [_vp, C.c_uint8, _vp]),
+        "dc_pos_to_cells": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint8)]),
+        "dc_pos_from_fen": (C.c_int, [C.c_char_p, _vp]),
+        "dc_move_pack": (C.c_uint16, [C.c_uint32] * 4),
+        "dc_validate_batch": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, _vp]),
+        "dc_apply_batch": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, _vp, _vp]),
+        "dc_replay": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, C.POINTER(_Stats)]),
+        "dc_replay_device": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp,
+                                       C.POINTER(_Stats)]),
+        "dc_gen_games": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                   _vp]),
+        "dc_gen_games_device": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                          C.c_uint32, _vp]),
+        "dc_perft": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, _vp, _vp, C.POINTER(C.c_uint32),
+                               C.POINTER(C.c_uint64)]),
+        "dc_perft_shard": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _vp,
+                                     _vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+        "dc_multi_perft": (C.c_int, [_vp, C.c_int, C.c_uint32, _vp, C.c_uint32, _vp, _vp, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint64)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype, f.argtypes = res, args
+    _LIB = L
+    return L
+
+
+def exported_symbols():
+    """Names the header declares; tests check the library exports each."""
+    hdr = os.path.join(os.path.dirname(os.path.dirname(PKG_DIR)), "include", "dchess.h")
+    import re
+    names = re.findall(r"^\s*(?:int|uint16_t|void\s*\*|const char\s*\*)\s+(dc_\w+)\s*\(", open(hdr).read(), re.M)
+    return sorted(set(names))
+
+
+def _check(status, what):
+    if status != SUCCESS:
+        raise DChessError(status, what)
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def verdict_message(v):
+    return lib().dc_verdict_message(v).decode()
+
+
+# ---------------------------------------------------------------- positions
+def startpos():
+    p = np.zeros(1, POS_DTYPE)
+    _check(lib().dc_startpos(_ptr(p)), "dc_startpos")
+    return p[0]
+
+
+def pos_from_cells(cells, turn):
+    cells = np.ascontiguousarray(cells, dtype=np.int8)
+    p = np.zeros(1, POS_DTYPE)
+    _check(lib().dc_pos_from_cells(_ptr(cells), int(turn), _ptr(p)), "dc_pos_from_cells")
+    return p[0]
+
+
+def pos_to_cells(pos):
+    p = np.array([pos], POS_DTYPE)
+    cells = np.zeros(64, np.int8)
+    turn = C.c_uint8()
+    _check(lib().dc_pos_to_cells(_ptr(p), _ptr(cells), C.byref(turn)), "dc_pos_to_cells")
+    return cells, turn.value
+
+
+def pos_from_fen(fen):
+    p = np.zeros(1, POS_DTYPE)
+    _check(lib().dc_pos_from_fen(fen.encode(), _ptr(p)), "dc_pos_from_fen")
+    return p[0]
+
+
+def move_pack(fx, fy, tx, ty):
+    return int(lib().dc_move_pack(fx, fy, tx, ty))
+
+
+class DeviceBuffer:
+    """Caller-owned device memory on an Engine's device (dc_device_alloc)."""
+
+    def __init__(self, engine, nbytes):
+        self.engine, self.nbytes = engine, int(nbytes)
+        p = _vp()
+        _check(lib().dc_device_alloc(engine.ctx, self.nbytes, C.byref(p)), "dc_device_alloc")
+        self.ptr = p
+
+    def upload(self, arr):
+        arr = np.ascontiguousarray(arr)
+        assert arr.nbytes <= self.nbytes
+        _check(lib().dc_memcpy_h2d(self.engine.ctx, self.ptr, _ptr(arr), arr.nbytes), "dc_memcpy_h2d")
+
+    def download(self, dtype, count):
+        out = np.empty(count, dtype)
+        assert out.nbytes <= self.nbytes
+        _check(lib().dc_memcpy_d2h(self.engine.ctx, _ptr(out), self.ptr, out.nbytes), "dc_memcpy_d2h")
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().dc_device_free(self.engine.ctx, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Engine:
+    """One dc_ctx: one gfx950 device, one HIP stream."""
+
+    def __init__(self, device=0):
+        ctx = _vp()
+        _check(lib().dc_ctx_create(int(device), C.byref(ctx)), f"dc_ctx_create({device})")
+        self.ctx = ctx
+        self.device = device
+
+    def close(self):
+        if self.ctx:
+            lib().dc_ctx_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -------------------------------------------------------------- timing
+    def set_profiling(self, on=True):
+        _check(lib().dc_ctx_set_profiling(self.ctx, 1 if on else 0), "dc_ctx_set_profiling")
+
+    def reset_stats(self):
+        _check(lib().dc_ctx_reset_stats(self.ctx), "dc_ctx_reset_stats")
+
+    def kernel_stats(self, name):
+        s = _KStats()
+        _check(lib().dc_ctx_kernel_stats(self.ctx, name.encode(), C.byref(s)), "dc_ctx_kernel_stats")
+        return {"launches": s.launches, "total_ms": s.total_ms, "units": s.units}
+
+    def alloc(self, nbytes):
+        return DeviceBuffer(self, nbytes)
+
+    # ---------------------------------------------------------- validation
+    def validate_batch(self, pos, moves, rules=RULES_REF):
+        pos = np.ascontiguousarray(pos, POS_DTYPE)
+        moves = np.ascontiguousarray(moves, np.uint16)
+        assert pos.shape == moves.shape
+        out = np.zeros(len(moves), np.uint8)
+        _check(lib().dc_validate_batch(self.ctx, rules, _ptr(pos), _ptr(moves), len(moves), _ptr(out)),
+               "dc_validate_batch")
+        return out
+
+    def apply_batch(self, pos, moves, rules=RULES_REF):
+        """Returns (new positions, verdicts, info)."""
+        pos = np.array(pos, POS_DTYPE, copy=True)
+        moves = np.ascontiguousarray(moves, np.uint16)
+        ver = np.zeros(len(moves), np.uint8)
+        info = np.zeros(len(moves), np.uint8)
+        _check(lib().dc_apply_batch(self.ctx, rules, _ptr(pos), _ptr(moves), len(moves), _ptr(ver), _ptr(info)),
+               "dc_apply_batch")
+        return pos, ver, info
+
+    # -------------------------------------------------------------- replay
+    def replay(self, moves, rules=RULES_REF, start=None, want_bitmap=True, want_digests=True):
+        """moves: uint16 [n_plies, n_games] ply-major.  Returns (bitmap, digests, stats dict)."""
+        moves = np.ascontiguousarray(moves, np.uint16)
+        n_plies, n_games = moves.shape
+        words = (n_games + 63) // 64
+        bitmap = np.zeros((n_plies, words), np.uint64) if want_bitmap else None
+        dig = np.zeros(n_games, np.uint64) if want_digests else None
+        st = _Stats()
+        sp = None
+        if start is not None:
+            sp = np.array([start], POS_DTYPE)
+        _check(lib().dc_replay(self.ctx, rules, _ptr(sp) if sp is not None else None, _ptr(moves), n_games, n_plies,
+                               _ptr(bitmap), _ptr(dig), C.byref(st)), "dc_replay")
+        return bitmap, dig, {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
+
+    def replay_device(self, d_moves, n_games, n_plies, d_bitmap=None, d_digests=None, rules=RULES_REF):
+        st = _Stats()
+        _check(lib().dc_replay_device(self.ctx, rules, None, d_moves.ptr, n_games, n_plies,
+                                      d_bitmap.ptr if d_bitmap else None, d_digests.ptr if d_digests else None,
+                                      C.byref(st)), "dc_replay_device")
+        return {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
+
+    def gen_games(self, seed, first_game, n_games, n_plies, noise_per_256=32, rules=RULES_REF):
+        out = np.zeros((n_plies, n_games), np.uint16)
+        _check(lib().dc_gen_games(self.ctx, rules, seed, first_game, n_games, n_plies, noise_per_256, _ptr(out)),
+               "dc_gen_games")
+        return out
+
+    def gen_games_device(self, d_out, seed, first_game, n_games, n_plies, noise_per_256=32, rules=RULES_REF):
+        _check(lib().dc_gen_games_device(self.ctx, rules, seed, first_game, n_games, n_plies, noise_per_256,
+                                         d_out.ptr), "dc_gen_games_device")
+
+    # --------------------------------------------------------------- perft
+    def perft(self, pos, depth, rules=RULES_REF):
+        """Returns (total, divide[n_root], root_moves[n_root])."""
+        p = np.array([pos], POS_DTYPE)
+        div = np.zeros(256, np.uint64)
+        rm = np.zeros(256, np.uint16)
+        nr, tot = C.c_uint32(), C.c_uint64()
+        _check(lib().dc_perft(self.ctx, rules, _ptr(p), depth, _ptr(div), _ptr(rm), C.byref(nr), C.byref(tot)),
+               "dc_perft")
+        return int(tot.value), div[:nr.value].copy(), rm[:nr.value].copy()
+
+    def perft_shard(self, pos, depth, split_depth, shard, n_shards, rules=RULES_REF):
+        p = np.array([pos], POS_DTYPE)
+        div = np.zeros(256, np.uint64)
+        rm = np.zeros(256, np.uint16)
+        nr, tot = C.c_uint32(), C.c_uint64()
+        _check(lib().dc_perft_shard(self.ctx, rules, _ptr(p), depth, split_depth, shard, n_shards, _ptr(div),
+                                    _ptr(rm), C.byref(nr), C.byref(tot)), "dc_perft_shard")
+        return int(tot.value), div[:nr.value].copy(), rm[:nr.value].copy()
+
+
+def multi_perft(devices, pos, depth, rules=RULES_REF):
+    devs = (C.c_int * len(devices))(*devices)
+    p = np.array([pos], POS_DTYPE)
+    div = np.zeros(256, np.uint64)
+    rm = np.zeros(256, np.uint16)
+    nr, tot = C.c_uint32(), C.c_uint64()
+    _check(lib().dc_multi_perft(devs, len(devices), rules, _ptr(p), depth, _ptr(div), _ptr(rm), C.byref(nr),
+                                C.byref(tot)), "dc_multi_perft")
+    return int(tot.value), div[:nr.value].copy(), rm[:nr.value].copy()
+
+
+# ---------------------------------------------------------------------------
+# Mirror of the reference's Rust surface (core/src/chess.rs), backed by the GPU.
+class AppError(Exception):
+    """AppError::InternalGameError(String) -- core/src/errors.rs:9."""
+
+
+class Position:
+    """proto query.Position{x, y} (core/proto/query.proto)."""
+
+    def __init__(self, x, y):
+        self.x, self.y = int(x), int(y)
+
+
+class Piece:
+    """proto game.Piece{color, kind} (core/proto/game.proto:15-18)."""
+
+    def __init__(self, color, kind):
+        self.color, self.kind = int(color), str(kind)
+
+    def __eq__(self, o):
+        return isinstance(o, Piece) and (self.color, self.kind) == (o.color, o.kind)
+
+    def __repr__(self):
+        return f"Piece({self.color}, {self.kind!r})"
+
+
+_DEFAULT_ENGINE = None
+
+
+def default_engine():
+    global _DEFAULT_ENGINE
+    if _DEFAULT_ENGINE is None:
+        _DEFAULT_ENGINE = Engine(0)
+    return _DEFAULT_ENGINE
+
+
+class GameState:
+    """GameState (core/proto/game.proto:7-13) with the chess.rs methods.
+
+    The board is kept as the proto's 8x8 grid of optional Pieces; every
+    validate/apply is one dc_validate_batch / dc_apply_batch call (n = 1).
+    """
+
+    def __init__(self, white_player, black_player, engine=None):  # chess.rs:12-20
+        self.white_player, self.black_player = white_player, black_player
+        self.turn = 0
+        self.history = ""
+        self.engine = engine or default_engine()
+        cells, _ = pos_to_cells(startpos())
+        self.board = [[None] * 8 for _ in range(8)]
+        for s in range(64):
+            if cells[s] >= 0:
+                self.board[s // 8][s % 8] = Piece(cells[s] >> 3, KINDS[cells[s] & 7])
+
+    def _pos(self):
+        cells = np.full(64, CELL_EMPTY, np.int8)
+        for x in range(8):
+            for y in range(8):
+                p = self.board[x][y]
+                if p is not None:
+                    k = KINDS.index(p.kind) if p.kind in KINDS[:6] else 6
+                    cells[8 * x + y] = p.color * 8 + k
+        return pos_from_cells(cells, self.turn)
+
+    def validate_move(self, frm, to):  # chess.rs:82-98
+        v = self.engine.validate_batch(np.array([self._pos()], POS_DTYPE),
+                                       np.array([move_pack(frm.x, frm.y, to.x, to.y)], np.uint16))[0]
+        if v == V_OOR:
+            raise IndexError("index out of bounds")  # the reference panics here
+        if v != V_OK:
+            raise AppError(verdict_message(v))
+
+    def apply_move(self, frm, to):  # chess.rs:43-80
+        pos = np.array([self._pos()], POS_DTYPE)
+        new, ver, info = self.engine.apply_batch(pos, np.array([move_pack(frm.x, frm.y, to.x, to.y)], np.uint16))
+        v = int(ver[0])
+        if v == V_OOR:
+            raise IndexError("index out of bounds")
+        if v != V_OK:
+            raise AppError(verdict_message(v))
+        kind, capture = KINDS[info[0] & 7], bool(info[0] & 8)
+        mover = self.board[frm.x][frm.y]
+        self._update_history(frm, to, mover.kind if kind == "X" else kind, capture)
+        cells, turn = pos_to_cells(new[0])
+        # Unknown-kind pieces never move (chess.rs:210): keep their original kind strings.
+        old = self.board
+        self.board = [[None] * 8 for _ in range(8)]
+        for s in range(64):
+            if cells[s] >= 0:
+                k = KINDS[cells[s] & 7]
+                if k == "X":
+                    k = old[s // 8][s % 8].kind
+                self.board[s // 8][s % 8] = Piece(cells[s] >> 3, k)
+        self.turn = turn
+
+    def _update_history(self, frm, to, kind, capture):  # chess.rs:127-184 (GPU supplies kind/capture)
+        san = "" if kind == "P" else kind
+        if capture:
+            if kind == "P":
+                san += chr(ord("a") + frm.y)
+            san += "x"
+        san += chr(ord("a") + to.y) + str(to.x + 1)
+        n = len(self.history.split())
+        self.history += ("" if n == 0 else " ") + f"{n + 1}. {san}"

@@ -1,0 +1,208 @@
+/*
+ * dchess.h -- C ABI of the MI355X chess state-transition engine.
+ *
+ * Drop-in boundary for the reference's move-validation call surface
+ * (dorlneylon/distributed-chess @ 2024-10-22, core/src/chess.rs):
+ *
+ *   reference (Rust inherent methods)                      replaced by
+ *   -----------------------------------------------------  ------------------------------
+ *   GameState::validate_move(&self,&Position,&Position)    dc_validate_batch (n >= 1)
+ *       core/src/chess.rs:82-98, called from
+ *       core/src/consensus/hotstuff.rs:138 (is_valid_tx)
+ *   GameState::apply_move(&mut self,Position,Position)     dc_apply_batch
+ *       core/src/chess.rs:43-80, called from
+ *       core/src/consensus/hotstuff.rs:52 (commit_block)
+ *   GameState::new / Board::new                            dc_startpos
+ *       core/src/chess.rs:12-20, :383-434
+ *   proto GameState.board (core/proto/game.proto:7-40)     dc_pos_from_cells / dc_pos_to_cells
+ *   Position{x,y} pairs (core/proto/query.proto:46-49)     dc_move_pack
+ *   AppError::InternalGameError(String)                    dc_verdict_message
+ *       core/src/errors.rs:9, strings chess.rs:104-121
+ *   (absent in the reference)                  dc_replay, dc_gen_games, dc_perft
+ *
+ * Conventions
+ *   - Every call returns int status: DC_SUCCESS (0) or a negative DC_E* code.
+ *     Nothing panics or aborts across the ABI; a rejected move is a verdict
+ *     (data), never an error.
+ *   - Buffers are caller-owned HOST memory unless the name ends in _device,
+ *     in which case they are device pointers on the context's device.
+ *   - A dc_ctx is bound to one device and one HIP stream and is not thread-safe:
+ *     use one context per thread.  Host-memory calls block until results are
+ *     on the host (wrap them in tokio::task::spawn_blocking on the Rust side).
+ *   - All arithmetic is integer; results are bit-exact with the reference.
+ *
+ * There is no CPU fallback behind this ABI: if no gfx950 device is present,
+ * dc_ctx_create fails with DC_ENODEV.
+ */
+#ifndef DCHESS_H
+#define DCHESS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ status */
+#define DC_SUCCESS 0
+#define DC_EINVAL (-1)       /* bad argument (null pointer, bad cell, bad turn, bad FEN) */
+#define DC_EHIP (-2)         /* HIP runtime failure */
+#define DC_ENOMEM (-3)       /* device or host allocation failed */
+#define DC_ENODEV (-4)       /* no usable gfx950 device */
+#define DC_ERCCL (-5)        /* RCCL failure (dc_multi_*) */
+#define DC_EUNSUPPORTED (-6) /* request outside what this build supports */
+
+/* ----------------------------------------------------------------- verdicts
+ * In the reference's check order (chess.rs:82-125), with OOR first because the
+ * reference indexes both squares before any rule check (chess.rs:85,92). */
+#define DC_V_OK 0
+#define DC_V_NO_PIECE 1   /* "No piece at the source location"     chess.rs:104-106 */
+#define DC_V_WRONG_TURN 2 /* "It's not this piece's turn to move"  chess.rs:113-115 */
+#define DC_V_ILLEGAL 3    /* "Invalid move for the piece"          chess.rs:119-121 */
+#define DC_V_OOR 4        /* coordinate >= 8: the reference panics (chess.rs:85,92) */
+
+/* ------------------------------------------------------------------- rules */
+#define DC_RULES_REF 0  /* bit-exact with core/src/chess.rs (geometry only) */
+#define DC_RULES_FIDE 1 /* standard chess: castling, en passant, promotion, no self-check */
+
+/* ---------------------------------------------------------------- position
+ * Quad-bitboard: square s = 8*x + y (x = row, 0 = White's back rank; y = column),
+ * the 4-bit nibble of square s is (bb[0]>>s &1) | (bb[1]>>s &1)<<1 | ... :
+ *   bb[0]            : 1 = black piece
+ *   bb[1],bb[2],bb[3]: bits 0,1,2 of the kind code
+ *                      P=1 N=2 K=3 OTHER=4 B=5 R=6 Q=7   (0 = empty square)
+ * so  diagonal sliders = bb[3]&bb[1], orthogonal sliders = bb[3]&bb[2].
+ * OTHER is a piece whose kind string is not one of "P","N","B","R","Q","K":
+ * it never moves (chess.rs:210) but blocks and can be captured.
+ * stm: side to move, 0 White / 1 Black (proto Color, game.proto:20-23).
+ * castle (FIDE): bit0 White O-O, bit1 White O-O-O, bit2 Black O-O, bit3 Black O-O-O.
+ * ep (FIDE): en-passant target square or -1.  Both are ignored under DC_RULES_REF. */
+typedef struct dc_pos {
+  uint64_t bb[4];
+  uint8_t stm;
+  uint8_t castle;
+  int8_t ep;
+  uint8_t reserved0;
+  uint32_t reserved1;
+} dc_pos; /* 40 bytes */
+
+/* -------------------------------------------------------------------- moves
+ * uint16: from | to<<6 | promo<<12, promo 0 none, 1 N, 2 B, 3 R, 4 Q (FIDE only;
+ * ignored under REF, where a Position pair carries no promotion).
+ * Bit 15 (DC_MOVE_OOR) marks a move with a coordinate >= 8: verdict DC_V_OOR.
+ * 0xFFFF (DC_MOVE_NONE) pads replay games that ended: skipped, not counted. */
+#define DC_MOVE_OOR 0x8000u
+#define DC_MOVE_NONE 0xFFFFu
+
+/* Cell encoding of dc_pos_from_cells / dc_pos_to_cells (the proto board flattened):
+ * cells[8*x+y] = -1 for an empty cell, else color*8 + kind with
+ * kind 0 P, 1 N, 2 B, 3 R, 4 Q, 5 K, 6 OTHER; color 0 White, 1 Black. */
+#define DC_CELL_EMPTY (-1)
+
+typedef struct dc_ctx dc_ctx;
+
+typedef struct dc_replay_stats {
+  uint64_t validated;  /* non-sentinel plies (accepted + rejected) */
+  uint64_t accepted;
+  uint64_t rejected;
+  uint64_t digest_sum; /* sum of per-game final-state digests (mod 2^64) */
+  uint64_t digest_xor; /* xor of per-game final-state digests */
+} dc_replay_stats;
+
+typedef struct dc_kernel_stats {
+  uint64_t launches;  /* launches of the kernel since the last reset */
+  double total_ms;    /* summed HIP-event duration of those launches */
+  uint64_t units;     /* work units those launches processed (leaves, moves, ...) */
+} dc_kernel_stats;
+
+/* ------------------------------------------------------------------ context */
+int dc_ctx_create(int device, dc_ctx** out);
+int dc_ctx_destroy(dc_ctx* ctx);
+int dc_ctx_device(const dc_ctx* ctx);
+/* hipStream_t of the context, as void* (so callers can order their own work). */
+void* dc_ctx_stream(dc_ctx* ctx);
+const char* dc_strerror(int status);
+/* Exact reference error text for verdicts 1..3 (chess.rs:104-121); "" for OK. */
+const char* dc_verdict_message(uint8_t verdict);
+int dc_version(void);
+
+/* Per-kernel HIP-event timing (enable, read, reset).  Kernel names:
+ * "validate", "replay", "gen_games", "expand_count", "expand_write", "count1", "count2". */
+int dc_ctx_set_profiling(dc_ctx* ctx, int enable);
+int dc_ctx_kernel_stats(dc_ctx* ctx, const char* kernel, dc_kernel_stats* out);
+int dc_ctx_reset_stats(dc_ctx* ctx);
+
+/* Device memory owned by the caller, on the context's device (for the *_device
+ * entry points, so a host program needs no other GPU runtime). */
+int dc_device_alloc(dc_ctx* ctx, size_t bytes, void** d_ptr);
+int dc_device_free(dc_ctx* ctx, void* d_ptr);
+int dc_memcpy_h2d(dc_ctx* ctx, void* d_dst, const void* src, size_t bytes);
+int dc_memcpy_d2h(dc_ctx* ctx, void* dst, const void* d_src, size_t bytes);
+
+/* ----------------------------------------------------------------- adapters
+ * Pure data-layout conversions on the host (no rule evaluation). */
+int dc_startpos(dc_pos* out); /* Board::new + turn White, chess.rs:12-20,383-434 */
+int dc_pos_from_cells(const int8_t cells[64], uint8_t turn, dc_pos* out);
+int dc_pos_to_cells(const dc_pos* pos, int8_t cells[64], uint8_t* turn);
+int dc_pos_from_fen(const char* fen, dc_pos* out);
+/* Position{x,y} pair -> move word; any coordinate >= 8 sets DC_MOVE_OOR. */
+uint16_t dc_move_pack(uint32_t from_x, uint32_t from_y, uint32_t to_x, uint32_t to_y);
+
+/* ------------------------------------------------------------- validation
+ * verdicts[i] = verdict of moves[i] in pos[i] (rules per call). */
+int dc_validate_batch(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, const uint16_t* moves, uint32_t n,
+                      uint8_t* verdicts);
+/* Validate and, where accepted, make the move in place (pos[i] updated, turn
+ * flipped); rejected positions are left untouched (chess.rs:44-46).
+ * info[i] (optional) = moved kind (cell kind 0..6) | 8 if the target held a piece,
+ * which is what update_history needs (chess.rs:156-167). */
+int dc_apply_batch(dc_ctx* ctx, uint32_t rules, dc_pos* pos, const uint16_t* moves, uint32_t n,
+                   uint8_t* verdicts, uint8_t* info);
+
+/* ------------------------------------------------------------------ replay
+ * Replays n_games games of n_plies ply-major moves (moves[ply*n_games + g])
+ * from *start (NULL = startpos).  Per ply: verdict; apply only if accepted
+ * (core/src/consensus/hotstuff.rs:52-56).  bitmap (optional) is ply-major
+ * [n_plies][ceil(n_games/64)] of accept bits; digests (optional) [n_games]. */
+int dc_replay(dc_ctx* ctx, uint32_t rules, const dc_pos* start, const uint16_t* moves, uint32_t n_games,
+              uint32_t n_plies, uint64_t* bitmap, uint64_t* digests, dc_replay_stats* stats);
+int dc_replay_device(dc_ctx* ctx, uint32_t rules, const dc_pos* start, const uint16_t* d_moves,
+                     uint32_t n_games, uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests,
+                     dc_replay_stats* stats);
+
+/* Seeded synthetic games: rng = splitmix64 from seed ^ game_id;
+ * per ply one draw r: (r & 0xFF) < noise_per_256 -> move (r>>8)&0xFFF, else the
+ * ((r>>32)*n>>32)-th legal move in (from, to, promo) order; no legal move ->
+ * DC_MOVE_NONE for the rest of the game.  Output ply-major [n_plies][n_games]. */
+int dc_gen_games(dc_ctx* ctx, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games,
+                 uint32_t n_plies, uint32_t noise_per_256, uint16_t* out);
+int dc_gen_games_device(dc_ctx* ctx, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games,
+                        uint32_t n_plies, uint32_t noise_per_256, uint16_t* d_out);
+
+/* -------------------------------------------------------------------- perft
+ * perft(pos, depth) = number of leaf nodes of the move tree (under
+ * REF the tree is every (from,to) pair validate_move accepts).  divide[i] is the
+ * count below root move root_moves[i]; both arrays need room for 256 entries
+ * (pass NULL to skip).  Root moves are in (from, to, promo) order. */
+int dc_perft(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint64_t* divide,
+             uint16_t* root_moves, uint32_t* n_root, uint64_t* total);
+/* One shard of perft for data-parallel runs: the frontier at ply `split_depth`
+ * is built deterministically, and this call counts only frontier nodes
+ * [shard*N/n_shards, (shard+1)*N/n_shards).  Summing divide[] over all shards
+ * (e.g. an RCCL all-reduce) gives dc_perft's result exactly. */
+int dc_perft_shard(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
+                   uint32_t shard, uint32_t n_shards, uint64_t* divide, uint16_t* root_moves,
+                   uint32_t* n_root, uint64_t* total);
+
+/* ------------------------------------------------------------- multi-GPU
+ * One process, n_devices GPUs, one RCCL communicator (ncclCommInitAll); the
+ * frontier is sharded contiguously and divide[] is combined with
+ * ncclAllReduce(ncclUint64, ncclSum) over xGMI. */
+int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_pos* pos, uint32_t depth,
+                   uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCHESS_H */

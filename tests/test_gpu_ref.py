@@ -1,0 +1,288 @@
+"""GPU parity tests for RULES_REF: every call goes through libdchess.so (C ABI)
+to the gfx950 kernels and is checked bit-exactly against the oracle (refcpu =
+literal restatement of core/src/chess.rs; fastcpu = independent engine) and
+the committed golden fixtures."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import dchess
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+KA = json.load(open(os.path.join(GOLD, "known_answers.json")))
+OG = json.load(open(os.path.join(GOLD, "oracle_golden.json")))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def pos_of(p):
+    """oracle Pos -> dc_pos record (via the ABI adapter)."""
+    d = dchess.pos_from_cells(p.cells, p.stm)
+    d["castle"], d["ep"] = p.castle, p.ep
+    return d
+
+
+# ------------------------------------------------------- reference unit tests
+def test_initial_game_state(engine):  # chess.rs:504-514
+    g = dchess.GameState("Alice", "Bob", engine)
+    assert g.turn == 0 and g.white_player == "Alice" and g.black_player == "Bob"
+
+
+def test_pawn_valid_move(engine):  # chess.rs:516-530
+    g = dchess.GameState("Alice", "Bob", engine)
+    g.validate_move(dchess.Position(1, 0), dchess.Position(3, 0))
+    g.turn = 1
+    g.validate_move(dchess.Position(6, 0), dchess.Position(5, 0))
+
+
+def test_rook_invalid_move(engine):  # chess.rs:532-539
+    g = dchess.GameState("Alice", "Bob", engine)
+    with pytest.raises(dchess.AppError):
+        g.validate_move(dchess.Position(0, 0), dchess.Position(2, 2))
+
+
+def test_turn_logic(engine):  # chess.rs:541-556
+    g = dchess.GameState("Alice", "Bob", engine)
+    g.turn = 0
+    g.validate_move(dchess.Position(1, 0), dchess.Position(2, 0))
+    g.turn = 1
+    g.validate_move(dchess.Position(6, 0), dchess.Position(5, 0))
+
+
+def test_error_strings_and_panic(engine):
+    g = dchess.GameState("Alice", "Bob", engine)
+    with pytest.raises(dchess.AppError, match="^No piece at the source location$"):
+        g.validate_move(dchess.Position(3, 3), dchess.Position(4, 3))
+    with pytest.raises(dchess.AppError, match="^It's not this piece's turn to move$"):
+        g.validate_move(dchess.Position(6, 0), dchess.Position(5, 0))
+    with pytest.raises(dchess.AppError, match="^Invalid move for the piece$"):
+        g.validate_move(dchess.Position(0, 2), dchess.Position(2, 4))
+    with pytest.raises(IndexError):
+        g.validate_move(dchess.Position(8, 0), dchess.Position(0, 0))
+
+
+def test_apply_history_sequence(engine):
+    seq = KA["apply_sequence"]
+    g = dchess.GameState("Alice", "Bob", engine)
+    for (f, t) in seq["moves"]:
+        g.apply_move(dchess.Position(*f), dchess.Position(*t))
+    assert g.history == seq["history"] and g.turn == seq["turn"]
+    assert g.board[3][2] == dchess.Piece(0, "B") and g.board[0][5] is None
+
+
+def test_known_answers_batch(engine):
+    s = dchess.startpos()
+    pos, moves, want = [], [], []
+    for c in KA["validate"]:
+        p = s.copy()
+        p["stm"] = c["turn"]
+        pos.append(p)
+        moves.append(dchess.move_pack(*c["from"], *c["to"]))
+        want.append(c["verdict"])
+    got = engine.validate_batch(np.array(pos, dchess.POS_DTYPE), np.array(moves, np.uint16))
+    assert got.tolist() == want
+
+
+# ------------------------------------------------- exhaustive (from,to) parity
+def _positions(n, seed):
+    mv = O.fast_gen_games(seed, 0, n, 90, noise_per_256=0)
+    rng = np.random.default_rng(seed)
+    out = []
+    for g in range(n):
+        p = O.Pos()
+        for ply in range(int(rng.integers(0, 90))):
+            m = int(mv[ply, g])
+            if m == O.SENTINEL:
+                break
+            if O.fast_validate(p, m) == O.OK:
+                p = O.fast_make(p, m)
+        out.append(p)
+    return out
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_validate_all_pairs_vs_refcpu(engine, seed):
+    ps = _positions(16, seed)
+    pos, moves, want = [], [], []
+    all_moves = np.array([f | (t << 6) for f in range(64) for t in range(64)], np.uint16)
+    for p in ps:
+        for stm in (0, 1):
+            q = p.copy()
+            q.stm = stm
+            d = pos_of(q)
+            pos.append(np.repeat(np.array([d], dchess.POS_DTYPE), 4096))
+            moves.append(all_moves)
+            want.append(O.ref_verdicts_all(q.cells, stm))
+    got = engine.validate_batch(np.concatenate(pos), np.concatenate(moves))
+    assert (got == np.concatenate(want)).all()
+
+
+def test_validate_odd_pieces_and_oor(engine):
+    rng = np.random.default_rng(5)
+    pos, moves, want = [], [], []
+    all_moves = np.array([f | (t << 6) for f in range(64) for t in range(64)], np.uint16)
+    for _ in range(6):
+        cells = np.full(64, -1, np.int8)
+        sq = rng.choice(64, 24, replace=False)
+        cells[sq] = rng.integers(0, 2, 24) * 8 + rng.integers(0, 7, 24)
+        for stm in (0, 1):
+            pos.append(np.repeat(np.array([dchess.pos_from_cells(cells, stm)], dchess.POS_DTYPE), 4096 + 2))
+            moves.append(np.concatenate([all_moves, np.array([dchess.MOVE_OOR, 0x8000 | 77], np.uint16)]))
+            want.append(np.concatenate([O.ref_verdicts_all(cells, stm), np.array([4, 4], np.uint8)]))
+    got = engine.validate_batch(np.concatenate(pos), np.concatenate(moves))
+    assert (got == np.concatenate(want)).all()
+
+
+def test_validate_empty_batch(engine):
+    assert engine.validate_batch(np.zeros(0, dchess.POS_DTYPE), np.zeros(0, np.uint16)).size == 0
+
+
+def test_apply_batch_vs_oracle(engine):
+    ps = _positions(64, 21)
+    pos, moves, exp_pos, exp_v = [], [], [], []
+    rng = np.random.default_rng(21)
+    for p in ps:
+        legal = O.fast_gen_moves(p)
+        for _ in range(4):
+            m = int(rng.choice(legal)) if (len(legal) and rng.random() < 0.7) else int(rng.integers(0, 4096))
+            v = O.fast_validate(p, m)
+            q = O.fast_make(p, m) if v == O.OK else p
+            pos.append(pos_of(p))
+            moves.append(m)
+            exp_v.append(v)
+            exp_pos.append(pos_of(q))
+    new, ver, info = engine.apply_batch(np.array(pos, dchess.POS_DTYPE), np.array(moves, np.uint16))
+    assert ver.tolist() == exp_v
+    exp = np.array(exp_pos, dchess.POS_DTYPE)
+    assert (new["bb"] == exp["bb"]).all() and (new["stm"] == exp["stm"]).all()
+    for i, m in enumerate(moves):
+        if exp_v[i] == 0:
+            cells, _ = dchess.pos_to_cells(pos[i])
+            f, t = m & 63, (m >> 6) & 63
+            assert info[i] == (cells[f] & 7) | (8 if cells[t] >= 0 else 0)
+
+
+# ------------------------------------------------------------ generator/replay
+def test_gen_games_matches_golden(engine):
+    g = OG["games"]
+    mv = engine.gen_games(g["seed"], g["first_game"], g["n_games"], g["n_plies"], g["noise_per_256"])
+    assert mv[:, 0].tolist() == g["first_game_moves"]
+    assert sha(mv) == g["moves_sha256"]
+    g2 = OG["games_noise"]
+    mv2 = engine.gen_games(g2["seed"], g2["first_game"], g2["n_games"], g2["n_plies"], g2["noise_per_256"])
+    assert sha(mv2) == g2["moves_sha256"]
+
+
+def test_replay_matches_golden(engine):
+    for key in ("games", "games_noise"):
+        g = OG[key]
+        mv = O.fast_gen_games(g["seed"], g["first_game"], g["n_games"], g["n_plies"], g["noise_per_256"])
+        bm, dg, st = engine.replay(mv)
+        assert sha(bm) == g["bitmap_sha256"] and sha(dg) == g["digests_sha256"]
+        assert st == g["stats"]
+
+
+@pytest.mark.parametrize("n_games,n_plies,noise", [(1, 1, 0), (63, 7, 32), (65, 81, 32), (1000, 80, 255), (4096, 3, 0)])
+def test_replay_ragged_vs_fastcpu(engine, n_games, n_plies, noise):
+    mv = O.fast_gen_games(7 + n_games, 3, n_games, n_plies, noise_per_256=noise)
+    bm, dg, st = engine.replay(mv)
+    fbm, fdg, fst = O.fast_replay(mv)
+    assert (bm == fbm).all() and (dg == fdg).all()
+    assert [st[k] for k in ("validated", "accepted", "rejected", "digest_sum", "digest_xor")] == [int(x) for x in fst]
+
+
+def test_replay_edge_cases(engine):
+    # no plies, sentinel-only games, out-of-range flagged moves, random junk words
+    bm, dg, st = engine.replay(np.zeros((0, 10), np.uint16))
+    assert st["validated"] == 0 and (dg == O.digest(O.startpos_cells(), 0)).all()
+    mv = np.full((5, 70), dchess.MOVE_NONE, np.uint16)
+    mv[2, ::3] = dchess.MOVE_OOR
+    mv[3, 1::2] = np.random.default_rng(1).integers(0, 0x7FFF, 35)
+    bm, dg, st = engine.replay(mv)
+    fbm, fdg, fst = O.fast_replay(mv)
+    assert (bm == fbm).all() and (dg == fdg).all() and st["validated"] == int(fst[0])
+
+
+def test_replay_vs_refcpu_sample(engine):
+    mv = engine.gen_games(0x5EED20241022, 123456, 512, 80, 32)
+    bm, dg, st = engine.replay(mv)
+    rbm, rdg, rst = O.ref_replay(mv, threads=8)
+    assert (bm == rbm).all() and (dg == rdg).all()
+
+
+def test_replay_device_large_properties(engine):
+    """1M games x 80 plies resident on the device: size-independent invariants."""
+    n, plies = 1 << 20, 80
+    d_moves = engine.alloc(n * plies * 2)
+    words = (n + 63) // 64
+    d_bm = engine.alloc(words * plies * 8)
+    d_dg = engine.alloc(n * 8)
+    engine.gen_games_device(d_moves, 0x5EED20241022, 0, n, plies, 32)
+    st = engine.replay_device(d_moves, n, plies, d_bm, d_dg)
+    bm = d_bm.download(np.uint64, words * plies)
+    dg = d_dg.download(np.uint64, n)
+    mv = d_moves.download(np.uint16, n * plies).reshape(plies, n)
+    assert st["validated"] == int((mv != dchess.MOVE_NONE).sum())
+    assert st["accepted"] == int(np.unpackbits(bm.view(np.uint8)).sum())
+    assert st["accepted"] + st["rejected"] == st["validated"]
+    assert st["digest_sum"] == int(dg.sum(dtype=np.uint64))
+    assert st["digest_xor"] == int(np.bitwise_xor.reduce(dg))
+    # spot-check a sample of games against the oracle
+    idx = np.arange(0, n, n // 256)
+    sub = np.ascontiguousarray(mv[:, idx])
+    _, fdg, _ = O.fast_replay(sub)
+    assert (fdg == dg[idx]).all()
+
+
+# ---------------------------------------------------------------------- perft
+@pytest.mark.parametrize("depth", [0, 1, 2, 3, 4, 5, 6])
+def test_perft_startpos_golden(engine, depth):
+    tot, div, rm = engine.perft(dchess.startpos(), depth)
+    if depth == 0:
+        assert tot == 1
+        return
+    g = OG["perft_ref"]["startpos"][str(depth)]
+    assert tot == g["total"]
+    assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+
+
+def test_perft_random_positions_golden(engine):
+    for e in OG["perft_ref"]["random_positions"]:
+        d = dchess.pos_from_cells(np.array(e["cells"], np.int8), e["stm"])
+        for depth in ("1", "2", "3", "4"):
+            assert engine.perft(d, int(depth))[0] == e["perft"][depth]
+
+
+def test_perft_vs_refcpu_odd_positions(engine):
+    rng = np.random.default_rng(9)
+    for _ in range(6):
+        cells = np.full(64, -1, np.int8)
+        sq = rng.choice(64, 18, replace=False)
+        cells[sq] = rng.integers(0, 2, 18) * 8 + rng.integers(0, 7, 18)
+        for stm in (0, 1):
+            want, _ = O.ref_perft(cells, stm, 2, threads=8)
+            assert engine.perft(dchess.pos_from_cells(cells, stm), 2)[0] == want
+            assert engine.perft(dchess.pos_from_cells(cells, stm), 3)[0] == \
+                O.fast_perft(O.Pos(cells, stm, 0, -1), 3)[0]
+
+
+@pytest.mark.parametrize("n_shards,split", [(2, 1), (3, 2), (8, 3), (5, 4)])
+def test_perft_shards_sum(engine, n_shards, split):
+    s = dchess.startpos()
+    tot, div, rm = engine.perft(s, 5)
+    acc = np.zeros_like(div)
+    t = 0
+    for k in range(n_shards):
+        st, sd, srm = engine.perft_shard(s, 5, split, k, n_shards)
+        assert (srm == rm).all()
+        acc += sd
+        t += st
+    assert t == tot and (acc == div).all()
