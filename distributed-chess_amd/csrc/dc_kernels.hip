@@ -1,4 +1,4 @@
-// dc_kernels.hip -- HIP kernels for gfx950 (RULES_REF), one lane per position/game.
+// dc_kernels.hip -- HIP kernels for gfx950 (RULES_REF and RULES_FIDE), one lane per position/game.
 //
 //   k_validate_ref   K2: one lane per (position, move)          -> verdict byte
 //   k_apply_ref      K2': validate + make in place               -> verdict, info
@@ -13,6 +13,8 @@
 //   k_scan_*         exclusive scan of child counts (u64 offsets)
 #include <hip/hip_runtime.h>
 
+#include "dc_fide.h"
+#include "dc_fide_rules.h"
 #include "dc_kernels.h"
 #include "dc_ref.h"
 
@@ -201,92 +203,255 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
   }
 }
 
-// -------------------------------------------------------------------- perft
-template <int STM>
-__global__ __launch_bounds__(256) void k_count_children(const Board* __restrict__ nodes, u32 n, u32* __restrict__ counts) {
+// ------------------------------------------------------------- FIDE (K1/K2/K5)
+__global__ __launch_bounds__(256) void k_validate_fide(const DevPos* __restrict__ pos, const uint16_t* __restrict__ moves,
+                                                       u32 n, uint8_t* __restrict__ out) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  counts[i] = ref_count<STM>(load_board(nodes, i));
+  const DevPos p = pos[i];
+  const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+  out[i] = (uint8_t)fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), moves[i]);
 }
 
-template <int STM>
-__global__ __launch_bounds__(256) void k_expand_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
-                                                      u32 n, const u64* __restrict__ offsets, Board* __restrict__ out,
-                                                      uint16_t* __restrict__ out_tags, uint16_t* __restrict__ out_moves,
-                                                      int root_level) {
+__global__ __launch_bounds__(256) void k_apply_fide(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 n,
+                                                    uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  DevPos p = pos[i];
+  Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+  const u32 m = moves[i];
+  const u32 meta = pack_meta(p.castle, p.ep);
+  const u32 v = fide_verdict(b, p.stm & 1, meta, m);
+  verdicts[i] = (uint8_t)v;
+  if (v != V_OK) {
+    if (info) info[i] = 0xFF;
+    return;
+  }
+  const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
+  if (info) {
+    const u32 code = nibble(b, f) >> 1;
+    const u32 cell_kind = (code == KC_P) ? 0 : (code == KC_N) ? 1 : (code == KC_B) ? 2 : (code == KC_R) ? 3
+                        : (code == KC_Q) ? 4 : (code == KC_K) ? 5 : 6;
+    info[i] = (uint8_t)(cell_kind | (((occupied(b) >> t) & 1) << 3));
+  }
+  const u32 nm = fide_make_rt(b, p.stm & 1, meta, f, t, (int)((m >> 12) & 7));
+  p.bb[0] = b.b0;
+  p.bb[1] = b.b1;
+  p.bb[2] = b.b2;
+  p.bb[3] = b.b3;
+  p.stm ^= 1;
+  p.castle = (uint8_t)(nm & 15);
+  p.ep = (nm & META_EP_VALID) ? (int8_t)((nm >> 4) & 63) : (int8_t)-1;
+  pos[i] = p;
+}
+
+__global__ __launch_bounds__(256) void k_replay_fide(Board start, u32 stm0, u32 meta0, const uint16_t* __restrict__ moves,
+                                                     u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
+                                                     u64* __restrict__ digests, u64* __restrict__ stats) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = g < n_games;
+  const u32 words = (n_games + 63) >> 6;
+  Board b = start;
+  u32 stm = stm0, meta = meta0;
+  u32 validated = 0, accepted = 0;
+  for (u32 ply = 0; ply < n_plies; ++ply) {
+    const u32 m = active ? moves[(size_t)ply * n_games + g] : 0xFFFFu;
+    bool ok = false;
+    if (m != 0xFFFFu) {
+      ++validated;
+      ok = fide_verdict(b, stm, meta, m) == V_OK;
+      if (ok) {
+        meta = fide_make_rt(b, stm, meta, (int)(m & 63), (int)((m >> 6) & 63), (int)((m >> 12) & 7));
+        stm ^= 1;
+        ++accepted;
+      }
+    }
+    const u64 word = ballot(ok);
+    if (bitmap && lane_id() == 0 && (g >> 6) < words) bitmap[(size_t)ply * words + (g >> 6)] = word;
+  }
+  u64 d = 0;
+  if (active) {
+    d = board_digest(b, stm);
+    if (digests) digests[g] = d;
+  }
+  const u64 sv = wave_sum64(validated), sa = wave_sum64(accepted), sd = wave_sum64(d);
+  u64 x = d;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x ^= __shfl_xor(x, o, 64);
+  if (lane_id() == 0 && stats) {
+    atomicAdd(stats + 0, sv);
+    atomicAdd(stats + 1, sa);
+    atomicAdd(stats + 2, sv - sa);
+    atomicAdd(stats + 3, sd);
+    atomicXor(stats + 4, x);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gen_games_fide(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
+                                                        u32 noise_per_256, uint16_t* __restrict__ out) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_games) return;
+  u64 s = seed ^ (first_game + g);
+  Board b{0, 0, 0, 0};
+  startpos_board(b);
+  u32 stm = 0, meta = CR_WK | CR_WQ | CR_BK | CR_BQ;
+  bool over = false;
+  for (u32 ply = 0; ply < n_plies; ++ply) {
+    uint16_t* slot = out + (size_t)ply * n_games + g;
+    if (over) {
+      *slot = 0xFFFF;
+      continue;
+    }
+    const u32 n = fide_count_rt(b, stm, meta);
+    if (n == 0) {
+      over = true;
+      *slot = 0xFFFF;
+      continue;
+    }
+    const u64 r = splitmix_next(s);
+    u32 m;
+    if ((u32)(r & 0xFF) < noise_per_256) m = (u32)((r >> 8) & 0xFFF);
+    else m = fide_kth_move(b, stm, meta, (u32)(((r >> 32) * (u64)n) >> 32));
+    *slot = (uint16_t)m;
+    if (fide_verdict(b, stm, meta, m) == V_OK) {
+      meta = fide_make_rt(b, stm, meta, (int)(m & 63), (int)((m >> 6) & 63), (int)((m >> 12) & 7));
+      stm ^= 1;
+    }
+  }
+}
+
+// -------------------------------------------------------------------- perft
+// Rules policies: the perft kernels are shared by RULES_REF and RULES_FIDE.
+struct RefRules {
+  static constexpr bool kMeta = false;
+  template <int STM>
+  __device__ static __forceinline__ u32 count(const Board& b, u32) { return ref_count<STM>(b); }
+  template <int STM, class V>
+  __device__ static __forceinline__ void for_each(const Board& b, u32, V&& v) {
+    ref_for_each_move<STM>(b, [&](int f, int t) { v(f, t, 0); });
+  }
+  template <int STM>
+  __device__ static __forceinline__ u32 make(Board& b, u32, int f, int t, int) {
+    ref_make(b, f, t);
+    return 0;
+  }
+};
+
+struct FideRules {
+  static constexpr bool kMeta = true;
+  template <int STM>
+  __device__ static __forceinline__ u32 count(const Board& b, u32 meta) { return fide_count<STM>(b, meta); }
+  template <int STM, class V>
+  __device__ static __forceinline__ void for_each(const Board& b, u32 meta, V&& v) {
+    fide_for_each_move<STM>(b, meta, v);
+  }
+  template <int STM>
+  __device__ static __forceinline__ u32 make(Board& b, u32 meta, int f, int t, int promo) {
+    return fide_make<STM>(b, meta, f, t, promo);
+  }
+};
+
+template <class R>
+__device__ __forceinline__ u32 load_meta(const uint16_t* meta, size_t i) {
+  if constexpr (R::kMeta) return meta[i];
+  else return 0;
+}
+
+template <class R, int STM>
+__global__ __launch_bounds__(256) void k_count_children(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                        u32 n, u32* __restrict__ counts) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  counts[i] = R::template count<STM>(load_board(nodes, i), load_meta<R>(meta, i));
+}
+
+template <class R, int STM>
+__global__ __launch_bounds__(256) void k_expand_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                      const uint16_t* __restrict__ tags, u32 n,
+                                                      const u64* __restrict__ offsets, Board* __restrict__ out,
+                                                      uint16_t* __restrict__ out_meta, uint16_t* __restrict__ out_tags,
+                                                      uint16_t* __restrict__ out_moves, int root_level) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const Board p = load_board(nodes, i);
+  const u32 pm = load_meta<R>(meta, i);
   const uint16_t tag = tags[i];
   u64 o = offsets[i];
   u32 j = 0;
-  ref_for_each_move<STM>(p, [&](int f, int t) {
+  R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
     Board c = p;
-    ref_make(c, f, t);
+    const u32 cm = R::template make<STM>(c, pm, f, t, promo);
     store_board(out, o, c);
+    if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
     out_tags[o] = root_level ? (uint16_t)j : tag;
-    if (out_moves) out_moves[o] = (uint16_t)(f | (t << 6));
+    if (out_moves) out_moves[o] = (uint16_t)(f | (t << 6) | (promo << 12));
     ++o;
     ++j;
   });
 }
 
-template <int STM>
-__global__ __launch_bounds__(256) void k_count1(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags, u32 n,
-                                                u64* __restrict__ divide) {
+template <class R, int STM>
+__global__ __launch_bounds__(256) void k_count1(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                const uint16_t* __restrict__ tags, u32 n, u64* __restrict__ divide) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
   const bool valid = i < n;
   u32 c = 0, tag = 0;
   if (valid) {
-    c = ref_count<STM>(load_board(nodes, i));
+    c = R::template count<STM>(load_board(nodes, i), load_meta<R>(meta, i));
     tag = tags[i];
   }
   accumulate_by_tag(divide, tag, c, valid);
 }
 
-// Fused last two plies.  Per wave: 64 parents -> their children's (from,to,
-// parent lane) are compacted into LDS at wave-prefix-sum offsets, then each
-// round every lane takes one child, makes it and bulk-counts the grandchildren.
+// Fused last two plies.  Per wave: 64 parents -> their children's (from, to,
+// promo, parent lane) are compacted into LDS at wave-prefix-sum offsets
+// (ballot/scan compaction), then each round every lane takes one child, makes
+// it and bulk-counts the grandchildren: no per-lane trip-count divergence.
 constexpr int kC2Waves = 4;
 constexpr int kC2Cap = 64 * 40;  // child slots per wave and window
 
 struct C2Shared {
   Board parent[kC2Waves][64];
+  u32 pmeta[kC2Waves][64];
   u32 slot[kC2Waves][kC2Cap];
 };
 
-template <int STM>
-__global__ __launch_bounds__(256) void k_count2(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags, u32 n,
-                                                u64* __restrict__ divide) {
+template <class R, int STM>
+__global__ __launch_bounds__(256) void k_count2(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                const uint16_t* __restrict__ tags, u32 n, u64* __restrict__ divide) {
   __shared__ C2Shared sh;
   const u32 w = threadIdx.x >> 6;
   const u32 lane = lane_id();
   Board* par = sh.parent[w];
+  u32* pmeta = sh.pmeta[w];
   u32* slot = sh.slot[w];
   const u32 groups = (n + 63) >> 6;
   for (u32 g = blockIdx.x * kC2Waves + w; g < groups; g += gridDim.x * kC2Waves) {
     const u32 i = (g << 6) + lane;
     const bool valid = i < n;
     Board p{0, 0, 0, 0};
-    u32 tag = 0;
+    u32 tag = 0, pm = 0;
     if (valid) {
       p = load_board(nodes, i);
+      pm = load_meta<R>(meta, i);
       tag = tags[i];
     }
-    const u32 cnt = valid ? ref_count<STM>(p) : 0;
+    const u32 cnt = valid ? R::template count<STM>(p, pm) : 0;
     const u32 incl = wave_incl_scan(cnt);
     const u32 excl = incl - cnt;
     const u32 total = __shfl(incl, 63, 64);
     const u64 vmask = ballot(valid);
     const u32 tag0 = __shfl(tag, lsb(vmask), 64);
     par[lane] = p;
+    if constexpr (R::kMeta) pmeta[lane] = pm;
     u64 acc = 0;  // grandchildren under parents whose tag == tag0
     for (u32 base = 0; base < total; base += kC2Cap) {
       wave_lds_sync();
       u32 j = excl;
       if (valid) {
-        ref_for_each_move<STM>(p, [&](int f, int t) {
-          if (j >= base && j - base < (u32)kC2Cap) slot[j - base] = (u32)f | ((u32)t << 6) | (lane << 12);
+        R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
+          if (j >= base && j - base < (u32)kC2Cap && j < excl + cnt)
+            slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (lane << 15);
           ++j;
         });
       }
@@ -296,10 +461,11 @@ __global__ __launch_bounds__(256) void k_count2(const Board* __restrict__ nodes,
         u32 k = 0, pl = 0;
         if (r < nslots) {
           const u32 e = slot[r];
-          pl = e >> 12;
+          pl = e >> 15;
           Board c = par[pl];
-          ref_make(c, (int)(e & 63), (int)((e >> 6) & 63));
-          k = ref_count<1 - STM>(c);
+          const u32 cm = R::template make<STM>(c, R::kMeta ? pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
+                                               (int)((e >> 12) & 7));
+          k = R::template count<1 - STM>(c, cm);
         }
         const u32 ptag = __shfl(tag, (int)pl, 64);
         if (ptag == tag0) acc += k;
@@ -404,42 +570,110 @@ hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_
   return hipGetLastError();
 }
 
-hipError_t launch_count_children(hipStream_t st, int stm, const Board* nodes, u32 n, u32* counts) {
+template <class R>
+static hipError_t count_children_impl(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, u32 n,
+                                      u32* counts) {
   if (n == 0) return hipSuccess;
-  if (stm) hipLaunchKernelGGL(k_count_children<1>, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, n, counts);
-  else hipLaunchKernelGGL(k_count_children<0>, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, n, counts);
+  if (stm) hipLaunchKernelGGL((k_count_children<R, 1>), dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, meta, n, counts);
+  else hipLaunchKernelGGL((k_count_children<R, 0>), dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, meta, n, counts);
   return hipGetLastError();
 }
 
-hipError_t launch_expand_write(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n,
-                               const u64* offsets, Board* out, uint16_t* out_tags, uint16_t* out_moves,
-                               int root_level) {
+template <class R>
+static hipError_t expand_write_impl(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta,
+                                    const uint16_t* tags, u32 n, const u64* offsets, Board* out, uint16_t* out_meta,
+                                    uint16_t* out_tags, uint16_t* out_moves, int root_level) {
   if (n == 0) return hipSuccess;
   if (stm)
-    hipLaunchKernelGGL(k_expand_write<1>, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, tags, n, offsets, out,
-                       out_tags, out_moves, root_level);
+    hipLaunchKernelGGL((k_expand_write<R, 1>), dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, meta, tags, n, offsets,
+                       out, out_meta, out_tags, out_moves, root_level);
   else
-    hipLaunchKernelGGL(k_expand_write<0>, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, tags, n, offsets, out,
-                       out_tags, out_moves, root_level);
+    hipLaunchKernelGGL((k_expand_write<R, 0>), dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, meta, tags, n, offsets,
+                       out, out_meta, out_tags, out_moves, root_level);
   return hipGetLastError();
 }
 
-hipError_t launch_count1(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide) {
+template <class R>
+static hipError_t count1_impl(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, const uint16_t* tags,
+                              u32 n, u64* divide) {
   if (n == 0) return hipSuccess;
-  if (stm) hipLaunchKernelGGL(k_count1<1>, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, tags, n, divide);
-  else hipLaunchKernelGGL(k_count1<0>, dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, tags, n, divide);
+  if (stm) hipLaunchKernelGGL((k_count1<R, 1>), dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, meta, tags, n, divide);
+  else hipLaunchKernelGGL((k_count1<R, 0>), dim3(blocks_for(n, 256)), dim3(256), 0, st, nodes, meta, tags, n, divide);
   return hipGetLastError();
 }
 
-hipError_t launch_count2(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide,
-                         u32 max_blocks) {
+template <class R>
+static hipError_t count2_impl(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, const uint16_t* tags,
+                              u32 n, u64* divide, u32 max_blocks) {
   if (n == 0) return hipSuccess;
   const u32 groups = (n + 63) / 64;
   u32 blocks = (groups + kC2Waves - 1) / kC2Waves;
   if (max_blocks && blocks > max_blocks) blocks = max_blocks;
-  if (stm) hipLaunchKernelGGL(k_count2<1>, dim3(blocks), dim3(256), 0, st, nodes, tags, n, divide);
-  else hipLaunchKernelGGL(k_count2<0>, dim3(blocks), dim3(256), 0, st, nodes, tags, n, divide);
+  if (stm) hipLaunchKernelGGL((k_count2<R, 1>), dim3(blocks), dim3(256), 0, st, nodes, meta, tags, n, divide);
+  else hipLaunchKernelGGL((k_count2<R, 0>), dim3(blocks), dim3(256), 0, st, nodes, meta, tags, n, divide);
   return hipGetLastError();
+}
+
+hipError_t launch_count_children(hipStream_t st, int stm, const Board* nodes, u32 n, u32* counts) {
+  return count_children_impl<RefRules>(st, stm, nodes, nullptr, n, counts);
+}
+hipError_t launch_expand_write(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n,
+                               const u64* offsets, Board* out, uint16_t* out_tags, uint16_t* out_moves,
+                               int root_level) {
+  return expand_write_impl<RefRules>(st, stm, nodes, nullptr, tags, n, offsets, out, nullptr, out_tags, out_moves,
+                                     root_level);
+}
+hipError_t launch_count1(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide) {
+  return count1_impl<RefRules>(st, stm, nodes, nullptr, tags, n, divide);
+}
+hipError_t launch_count2(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide,
+                         u32 max_blocks) {
+  return count2_impl<RefRules>(st, stm, nodes, nullptr, tags, n, divide, max_blocks);
+}
+
+hipError_t launch_validate_fide(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_validate_fide, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, out);
+  return hipGetLastError();
+}
+hipError_t launch_apply_fide(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
+                             uint8_t* info) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_apply_fide, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, verdicts, info);
+  return hipGetLastError();
+}
+hipError_t launch_replay_fide(hipStream_t st, const DevPos& start, const uint16_t* moves, u32 n_games, u32 n_plies,
+                              u64* bitmap, u64* digests, u64* stats) {
+  if (n_games == 0) return hipSuccess;
+  const Board b{start.bb[0], start.bb[1], start.bb[2], start.bb[3]};
+  hipLaunchKernelGGL(k_replay_fide, dim3(blocks_for(n_games, 256)), dim3(256), 0, st, b, (u32)(start.stm & 1),
+                     (u32)pack_meta(start.castle, start.ep), moves, n_games, n_plies, bitmap, digests, stats);
+  return hipGetLastError();
+}
+hipError_t launch_gen_games_fide(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
+                                 uint16_t* out) {
+  if (n_games == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gen_games_fide, dim3(blocks_for(n_games, 256)), dim3(256), 0, st, seed, first_game, n_games,
+                     n_plies, noise, out);
+  return hipGetLastError();
+}
+hipError_t launch_count_children_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, u32 n,
+                                      u32* counts) {
+  return count_children_impl<FideRules>(st, stm, nodes, meta, n, counts);
+}
+hipError_t launch_expand_write_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta,
+                                    const uint16_t* tags, u32 n, const u64* offsets, Board* out, uint16_t* out_meta,
+                                    uint16_t* out_tags, uint16_t* out_moves, int root_level) {
+  return expand_write_impl<FideRules>(st, stm, nodes, meta, tags, n, offsets, out, out_meta, out_tags, out_moves,
+                                      root_level);
+}
+hipError_t launch_count1_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, const uint16_t* tags,
+                              u32 n, u64* divide) {
+  return count1_impl<FideRules>(st, stm, nodes, meta, tags, n, divide);
+}
+hipError_t launch_count2_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, const uint16_t* tags,
+                              u32 n, u64* divide, u32 max_blocks) {
+  return count2_impl<FideRules>(st, stm, nodes, meta, tags, n, divide, max_blocks);
 }
 
 size_t scan_temp_elems(u64 n) {

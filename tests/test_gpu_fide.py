@@ -1,0 +1,101 @@
+"""GPU parity tests for RULES_FIDE (standard chess: castling, en passant,
+promotion, no self-check).  The reference validator does not implement these
+rules, so the pins are the published perft tables
+(tests/golden/oracle_golden.json "perft_fide") and the independent fastcpu
+mailbox engine."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import dchess
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+OG = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))
+FIDE = dchess.RULES_FIDE
+DEPTHS = {"startpos": 5, "kiwipete": 4, "pos3": 5, "pos4": 4, "pos5": 4, "pos6": 4}
+
+
+def dpos(p):
+    d = dchess.pos_from_cells(p.cells, p.stm)
+    d["castle"], d["ep"] = p.castle, p.ep
+    return d
+
+
+@pytest.mark.parametrize("name", list(DEPTHS))
+def test_perft_suite_published(engine, name):
+    e = OG["perft_fide"][name]
+    pos = dchess.pos_from_fen(e["fen"])
+    for d in range(1, DEPTHS[name] + 1):
+        tot, div, rm = engine.perft(pos, d, rules=FIDE)
+        assert tot == e["perft"][str(d)], (name, d)
+        if d <= 3:
+            ot, od, orm = O.fast_perft(O.Pos.from_fen(e["fen"]), d, O.FIDE)
+            assert dict(zip(rm.tolist(), div.tolist())) == dict(zip(orm.tolist(), od.tolist()))
+
+
+def _fide_positions(n, seed):
+    mv = O.fast_gen_games(seed, 0, n, 120, noise_per_256=0, rules=O.FIDE)
+    rng = np.random.default_rng(seed)
+    out = []
+    for g in range(n):
+        p = O.Pos()
+        for ply in range(int(rng.integers(0, 120))):
+            m = int(mv[ply, g])
+            if m == O.SENTINEL:
+                break
+            if O.fast_validate(p, m, O.FIDE) == O.OK:
+                p = O.fast_make(p, m, O.FIDE)
+        out.append(p)
+    # plus the suite positions (castling / ep / promotion rich)
+    out += [O.Pos.from_fen(e["fen"]) for e in OG["perft_fide"].values()]
+    return out
+
+
+def test_perft_random_fide_positions(engine):
+    for p in _fide_positions(24, 31):
+        for d in (1, 2, 3):
+            assert engine.perft(dpos(p), d, rules=FIDE)[0] == O.fast_perft(p, d, O.FIDE)[0]
+
+
+def test_validate_all_pairs_fide(engine):
+    ps = _fide_positions(20, 41)
+    base = np.array([f | (t << 6) for f in range(64) for t in range(64)], np.uint16)
+    pos, moves, want = [], [], []
+    for p in ps:
+        legal = O.fast_gen_moves(p, O.FIDE)
+        extra = np.array(sorted(set(int(m) for m in legal if m >> 12)) + [int(m) ^ (1 << 12) for m in legal if m >> 12]
+                         + [0x8000], np.uint16)
+        mv = np.concatenate([base, extra])
+        pos.append(np.repeat(np.array([dpos(p)], dchess.POS_DTYPE), len(mv)))
+        moves.append(mv)
+        want.append(np.array([O.fast_validate(p, int(m), O.FIDE) for m in mv], np.uint8))
+    got = engine.validate_batch(np.concatenate(pos), np.concatenate(moves), rules=FIDE)
+    assert (got == np.concatenate(want)).all()
+
+
+def test_apply_fide_vs_oracle(engine):
+    ps = _fide_positions(40, 51)
+    pos, moves, exp = [], [], []
+    for p in ps:
+        for m in O.fast_gen_moves(p, O.FIDE)[:12]:
+            pos.append(dpos(p))
+            moves.append(int(m))
+            exp.append(dpos(O.fast_make(p, int(m), O.FIDE)))
+    new, ver, _ = engine.apply_batch(np.array(pos, dchess.POS_DTYPE), np.array(moves, np.uint16), rules=FIDE)
+    e = np.array(exp, dchess.POS_DTYPE)
+    assert (ver == 0).all()
+    assert (new["bb"] == e["bb"]).all() and (new["stm"] == e["stm"]).all()
+    assert (new["castle"] == e["castle"]).all() and (new["ep"] == e["ep"]).all()
+
+
+def test_gen_and_replay_fide(engine):
+    mv = engine.gen_games(777, 10, 300, 120, 32, rules=FIDE)
+    omv = O.fast_gen_games(777, 10, 300, 120, noise_per_256=32, rules=O.FIDE)
+    assert (mv == omv).all()
+    bm, dg, st = engine.replay(mv, rules=FIDE)
+    fbm, fdg, fst = O.fast_replay(mv, rules=O.FIDE)
+    assert (bm == fbm).all() and (dg == fdg).all() and st["accepted"] == int(fst[1])
