@@ -116,10 +116,10 @@ def cpu_baselines(args, threads):
                                      f"(from,to) pairs per node) perft(startpos,4) = {leaves} leaves in {dt:.2f}s",
                            "host_cpus": os.cpu_count()}
     t0 = time.perf_counter()
-    fl, _, _ = O.fast_perft(O.Pos(), 5, O.REF, threads=threads)
+    fl, _, _ = O.fast_perft(O.Pos(), args.depth, O.REF, threads=threads)
     dt = time.perf_counter() - t0
     out["cpu_fast"] = {"value": fl / dt, "unit": "leaf nodes/s", "cores": threads, "kind": "port",
-                       "sample": f"fastcpu mailbox engine perft(startpos,5) = {fl} leaves in {dt:.2f}s"}
+                       "sample": f"fastcpu mailbox engine (bulk counting) perft(startpos,{args.depth}) = {fl} leaves in {dt:.2f}s"}
     if not args.no_replay:
         n = 20_000
         mv = O.fast_gen_games(0x5EED20241022, 0, n, args.plies, 32, threads=threads)
