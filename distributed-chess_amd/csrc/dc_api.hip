@@ -19,6 +19,7 @@
 #include "../../include/dchess.h"
 #include "dc_fide.h"
 #include "dc_kernels.h"
+#include "dc_perft.h"
 
 using dc::Board;
 using dc::DevPos;
@@ -74,15 +75,25 @@ struct dc_ctx {
   std::vector<PendingEvent> pending;
   std::map<std::string, KStat> stats;
 
-  // perft frontier (ping-pong) and scratch
+  // perft frontier (ping-pong), top-level scratch and per-run control block
   DBuf<Board> nodes[2];
   DBuf<uint16_t> tags[2];
   DBuf<uint16_t> meta[2];  // FIDE castle/ep per node
-  DBuf<uint16_t> root_moves;
+  DBuf<Board> top_nodes;
+  DBuf<uint16_t> top_tags, top_meta;
   DBuf<u32> counts;
   DBuf<u64> offsets;
   DBuf<u64> scan_tmp;
-  DBuf<u64> divide;
+  DBuf<dc::PerftResult> res;
+  DBuf<dc::Range> rng;
+  DBuf<u64> desc;
+  DBuf<Board> root;
+  DBuf<uint16_t> root_meta;
+  dc::PerftResult* res_host = nullptr;  // pinned
+  struct RootStage {
+    Board b;
+    uint16_t meta;
+  }* root_host = nullptr;  // pinned
   // batch / replay scratch
   DBuf<DevPos> pos;
   DBuf<uint16_t> moves;
@@ -90,12 +101,16 @@ struct dc_ctx {
   DBuf<u64> bitmap, digests, stats5;
 
   ~dc_ctx() {
-    for (auto* b : {&nodes[0], &nodes[1]}) b->release();
-    for (auto* b : {&tags[0], &tags[1], &meta[0], &meta[1], &root_moves, &moves}) b->release();
+    for (auto* b : {&nodes[0], &nodes[1], &top_nodes, &root}) b->release();
+    for (auto* b : {&tags[0], &tags[1], &meta[0], &meta[1], &top_tags, &top_meta, &root_meta, &moves}) b->release();
     counts.release();
     offsets.release();
     scan_tmp.release();
-    divide.release();
+    res.release();
+    rng.release();
+    desc.release();
+    if (res_host) (void)hipHostFree(res_host);
+    if (root_host) (void)hipHostFree(root_host);
     pos.release();
     verdicts.release();
     info.release();
@@ -450,14 +465,16 @@ static int replay_impl(dc_ctx* c, uint32_t rules, const dc_pos* start, const uin
   if (start) s = *start;
   else dc_startpos(&s);
   if (s.stm > 1) return DC_EINVAL;
-  HIP_TRY(c->stats5.ensure(5));
+  HIP_TRY(c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(std::max<u32>(n_games, 1))));
   HIP_TRY(hipMemsetAsync(c->stats5.p, 0, 5 * sizeof(u64), c->stream));
+  u64* partial = c->stats5.p + 5;
   const Board b{s.bb[0], s.bb[1], s.bb[2], s.bb[3]};
   HIP_TRY(c->timed("replay", (u64)n_games * n_plies, [&] {
     return rules == DC_RULES_REF
-               ? dc::launch_replay_ref(c->stream, b, s.stm, d_moves, n_games, n_plies, d_bitmap, d_digests, c->stats5.p)
+               ? dc::launch_replay_ref(c->stream, b, s.stm, d_moves, n_games, n_plies, d_bitmap, d_digests, c->stats5.p,
+                                       partial)
                : dc::launch_replay_fide(c->stream, reinterpret_cast<const DevPos&>(s), d_moves, n_games, n_plies,
-                                        d_bitmap, d_digests, c->stats5.p);
+                                        d_bitmap, d_digests, c->stats5.p, partial);
   }));
   u64 h[5];
   HIP_TRY(hipMemcpyAsync(h, c->stats5.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
@@ -535,51 +552,150 @@ int dc_gen_games(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first_game, 
 }  // extern "C"
 
 // =================================================================== perft
-// Level-synchronous, deterministic frontier: level L+1 = children of level L in
-// (parent, move-class, target) order, so every rank that rebuilds the top levels
-// sees the same frontier and can take a contiguous shard of it.  The last two
-// plies are fused into k_count2 (or the last ply into k_count1).
+// Device-driven level pipeline (dc_perft.hip): the level sizes live in device
+// Range descriptors, capacities are bounded on the host (n_bound x 64 children,
+// within kSpecBudget bytes per level), and the host synchronises once at the
+// end.  Writes past a capacity are dropped and flagged; the run is then
+// repeated in exact mode, which reads every level size back before sizing the
+// next (one sync per level).  Level order is deterministic, so ranks that
+// rebuild the top levels agree on the frontier and take contiguous shards.
 namespace {
 
-struct Level {
-  Board* nodes;
-  uint16_t* tags;
-  uint16_t* meta;
-  u64 n;
-};
+constexpr u64 kBranchBound = 64;                    // speculative children per node
+constexpr u64 kSpecBudget = 4ull << 30;             // bytes per speculative level
+constexpr u64 kNodeBytes = sizeof(Board) + 2 * sizeof(uint16_t);
+constexpr u64 kDescMaxParents = 1ull << 21;       // final levels up to this size use the descriptor path
 
-int expand_level(dc_ctx* c, uint32_t rules, int stm, const Level& in, int dst, bool root, Level* out) {
-  const u32 n = (u32)in.n;
-  HIP_TRY(c->counts.ensure(std::max<u64>(in.n, 1)));
-  HIP_TRY(c->offsets.ensure(std::max<u64>(in.n, 1)));
-  HIP_TRY(c->scan_tmp.ensure(dc::scan_temp_elems(in.n)));
-  HIP_TRY(c->timed("expand_count", in.n, [&] {
-    return rules == DC_RULES_REF ? dc::launch_count_children(c->stream, stm, in.nodes, n, c->counts.p)
-                                 : dc::launch_count_children_fide(c->stream, stm, in.nodes, in.meta, n, c->counts.p);
+int ensure_level(dc_ctx* c, int b, u64 n, bool fide) {
+  const size_t want = std::max<u64>(n, 1);
+  HIP_TRY(c->nodes[b].ensure(want));
+  HIP_TRY(c->tags[b].ensure(want));
+  if (fide) HIP_TRY(c->meta[b].ensure(want));
+  return DC_SUCCESS;
+}
+
+int read_range(dc_ctx* c, int level, u64* n) {
+  dc::Range r;
+  HIP_TRY(hipMemcpyAsync(&r, c->rng.p + level, sizeof r, hipMemcpyDeviceToHost, c->stream));
+  int e = sync_ctx(c);
+  if (e != DC_SUCCESS) return e;
+  *n = r.hi - r.lo;
+  return DC_SUCCESS;
+}
+
+int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
+              uint32_t n_shards, bool exact, dc::PerftResult* out) {
+  const bool fide = rules == DC_RULES_FIDE;
+  const bool sharded = n_shards > 1;
+  const u32 F = depth >= 3 ? depth - 2 : 1;       // level handed to the final kernel
+  const int final_plies = depth >= 3 ? 2 : 1;     // depth 1: no final kernel
+  const u32 S = std::max<u32>(1, std::min(split_depth, F));
+  u32 T = exact ? 1 : std::min<u32>(F, 2);        // levels built by the single-workgroup top kernel
+  if (sharded) T = std::min(T, S);
+  // buffers (allocated before anything is enqueued)
+  if (!c->res_host) HIP_TRY(hipHostMalloc((void**)&c->res_host, sizeof(dc::PerftResult)));
+  if (!c->root_host) HIP_TRY(hipHostMalloc((void**)&c->root_host, sizeof(*c->root_host)));
+  HIP_TRY(c->res.ensure(1));
+  HIP_TRY(c->rng.ensure(16));
+  HIP_TRY(c->root.ensure(1));
+  HIP_TRY(c->root_meta.ensure(1));
+  HIP_TRY(c->top_nodes.ensure(256));
+  HIP_TRY(c->top_tags.ensure(256));
+  if (fide) HIP_TRY(c->top_meta.ensure(256));
+  const u64 cap_T = T == 1 ? 256 : 256 * 256;
+  int e = ensure_level(c, 0, cap_T, fide);
+  if (e != DC_SUCCESS) return e;
+  // root upload from pinned memory, result block cleared
+  c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
+  c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
+  HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemsetAsync(c->res.p, 0, sizeof(dc::PerftResult), c->stream));
+  HIP_TRY(c->timed("expand_top", 0, [&] {
+    return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, c->top_nodes.p,
+                                 c->top_meta.p, c->top_tags.p, 256, c->nodes[0].p, c->meta[0].p, c->tags[0].p, cap_T,
+                                 c->res.p, c->rng.p + T);
   }));
-  HIP_TRY(dc::launch_scan_u32(c->stream, c->counts.p, in.n, c->offsets.p, c->scan_tmp.p));
-  u64 last_off = 0;
-  u32 last_cnt = 0;
-  HIP_TRY(hipMemcpyAsync(&last_off, c->offsets.p + (in.n - 1), sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipMemcpyAsync(&last_cnt, c->counts.p + (in.n - 1), sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-  int r = sync_ctx(c);
-  if (r != DC_SUCCESS) return r;
-  const u64 total = last_off + last_cnt;
-  if (total > 0xFFFFFFFFull) return DC_EUNSUPPORTED;  // frontier > 2^32 nodes: deeper split needed
-  const size_t want = std::max<u64>(total, 1);
-  HIP_TRY(c->nodes[dst].ensure(want));
-  HIP_TRY(c->tags[dst].ensure(want));
-  if (rules == DC_RULES_FIDE) HIP_TRY(c->meta[dst].ensure(want));
-  if (root) HIP_TRY(c->root_moves.ensure(std::max<u64>(total, 1)));
-  HIP_TRY(c->timed("expand_write", total, [&] {
-    return rules == DC_RULES_REF
-               ? dc::launch_expand_write(c->stream, stm, in.nodes, in.tags, n, c->offsets.p, c->nodes[dst].p,
-                                         c->tags[dst].p, root ? c->root_moves.p : nullptr, root ? 1 : 0)
-               : dc::launch_expand_write_fide(c->stream, stm, in.nodes, in.meta, in.tags, n, c->offsets.p,
-                                              c->nodes[dst].p, c->meta[dst].p, c->tags[dst].p,
-                                              root ? c->root_moves.p : nullptr, root ? 1 : 0);
-  }));
-  *out = Level{c->nodes[dst].p, c->tags[dst].p, rules == DC_RULES_FIDE ? c->meta[dst].p : nullptr, total};
+  u32 L = T;
+  u64 nb = cap_T;
+  int buf = 0;
+  if (sharded && L == S) HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
+  while (L < F) {
+    const int stm = pos->stm ^ (L & 1);
+    bool exact_level = exact || nb * kBranchBound * kNodeBytes > kSpecBudget;
+    if (exact_level) {
+      e = read_range(c, L, &nb);
+      if (e != DC_SUCCESS) return e;
+    }
+    u64 cap_next = nb * kBranchBound;
+    HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
+    HIP_TRY(c->offsets.ensure(std::max<u64>(nb, 1)));
+    HIP_TRY(c->scan_tmp.ensure(dc::scan_temp_elems(std::max<u64>(nb, 1))));
+    const Board* in = c->nodes[buf].p;
+    const uint16_t* in_meta = fide ? c->meta[buf].p : nullptr;
+    const uint16_t* in_tags = c->tags[buf].p;
+    HIP_TRY(c->timed("expand_count", 0, [&] {
+      return dc::launch_count_children(c->stream, rules, stm, in, in_meta, c->rng.p + L, nb, c->counts.p);
+    }));
+    exact_level = exact_level && (exact || cap_next * kNodeBytes > kSpecBudget);
+    HIP_TRY(c->timed("scan", 0, [&] {
+      return dc::launch_scan_level(c->stream, c->counts.p, c->rng.p + L, nb, c->offsets.p, c->scan_tmp.p,
+                                   c->rng.p + L + 1, exact_level ? ~0ull : cap_next, c->res.p);
+    }));
+    if (exact_level) {
+      e = read_range(c, L + 1, &cap_next);
+      if (e != DC_SUCCESS) return e;
+      if (cap_next > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
+    }
+    e = ensure_level(c, buf ^ 1, cap_next, fide);
+    if (e != DC_SUCCESS) return e;
+    HIP_TRY(c->timed("expand_write", 0, [&] {
+      return dc::launch_expand_write(c->stream, rules, stm, in, in_meta, in_tags, c->rng.p + L, nb, c->offsets.p,
+                                     c->nodes[buf ^ 1].p, fide ? c->meta[buf ^ 1].p : nullptr, c->tags[buf ^ 1].p,
+                                     cap_next);
+    }));
+    buf ^= 1;
+    ++L;
+    nb = cap_next;
+    if (sharded && L == S) HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
+  }
+  const u64 desc_cap = nb * kBranchBound;
+  const bool use_desc = depth >= 3 && !exact && nb <= kDescMaxParents && desc_cap * sizeof(u64) <= kSpecBudget;
+  if (use_desc) {
+    // final level F: children as descriptors (count, scan into Range slot F+1, emit), then one lane per child
+    const int stm = pos->stm ^ (L & 1);
+    const Board* in = c->nodes[buf].p;
+    const uint16_t* in_meta = fide ? c->meta[buf].p : nullptr;
+    HIP_TRY(c->desc.ensure(std::max<u64>(desc_cap, 1)));
+    HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
+    HIP_TRY(c->offsets.ensure(std::max<u64>(nb, 1)));
+    HIP_TRY(c->scan_tmp.ensure(dc::scan_temp_elems(std::max<u64>(nb, 1))));
+    HIP_TRY(c->timed("expand_count", 0, [&] {
+      return dc::launch_count_children(c->stream, rules, stm, in, in_meta, c->rng.p + L, nb, c->counts.p);
+    }));
+    HIP_TRY(c->timed("scan", 0, [&] {
+      return dc::launch_scan_level(c->stream, c->counts.p, c->rng.p + L, nb, c->offsets.p, c->scan_tmp.p,
+                                   c->rng.p + L + 1, desc_cap, c->res.p);
+    }));
+    HIP_TRY(c->timed("emit_desc", 0, [&] {
+      return dc::launch_emit_desc(c->stream, rules, stm, in, in_meta, c->rng.p + L, nb, c->offsets.p, c->desc.p,
+                                  desc_cap);
+    }));
+    HIP_TRY(c->timed("count2", 0, [&] {
+      return dc::launch_count_desc(c->stream, rules, stm, in, in_meta, c->tags[buf].p, c->desc.p, c->rng.p + L + 1,
+                                   desc_cap, c->res.p->divide);
+    }));
+  } else if (depth >= 2) {
+    const int stm = pos->stm ^ (L & 1);
+    HIP_TRY(c->timed(final_plies == 2 ? "count2" : "count1", 0, [&] {
+      return dc::launch_final(c->stream, rules, stm, final_plies, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
+                              c->tags[buf].p, c->rng.p + L, nb, c->res.p->divide);
+    }));
+  }
+  HIP_TRY(hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream));
+  e = sync_ctx(c);
+  if (e != DC_SUCCESS) return e;
+  *out = *c->res_host;
   return DC_SUCCESS;
 }
 
@@ -593,91 +709,25 @@ int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uin
     *total = (shard == 0) ? 1 : 0;
     return DC_SUCCESS;
   }
-  // level 0: the root
-  HIP_TRY(c->nodes[0].ensure(1));
-  HIP_TRY(c->tags[0].ensure(1));
-  HIP_TRY(c->meta[0].ensure(1));
-  const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
-  const uint16_t zero = 0;
-  const uint16_t rmeta = dc::pack_meta(pos->castle, pos->ep);
-  HIP_TRY(hipMemcpyAsync(c->nodes[0].p, &rb, sizeof rb, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->tags[0].p, &zero, sizeof zero, hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->meta[0].p, &rmeta, sizeof rmeta, hipMemcpyHostToDevice, c->stream));
-  Level cur{c->nodes[0].p, c->tags[0].p, rules == DC_RULES_FIDE ? c->meta[0].p : nullptr, 1};
-  Level nxt;
-  int r = expand_level(c, rules, pos->stm, cur, 1, true, &nxt);
-  if (r != DC_SUCCESS) return r;
-  cur = nxt;
-  const u32 nr = (u32)cur.n;
-  if (nr > 256) return DC_EUNSUPPORTED;
+  dc::PerftResult r;
+  int e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r);
+  if (e == DC_SUCCESS && r.overflow) e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, true, &r);
+  if (e != DC_SUCCESS) return e;
+  if (r.overflow) return DC_EUNSUPPORTED;  // more than 256 root moves, or a level beyond 2^32 nodes
+  const u32 nr = r.n_root;
   if (n_root) *n_root = nr;
-  std::vector<uint16_t> rm(nr);
-  if (nr) HIP_TRY(hipMemcpyAsync(rm.data(), c->root_moves.p, nr * sizeof(uint16_t), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(c->divide.ensure(256));
-  HIP_TRY(hipMemsetAsync(c->divide.p, 0, 256 * sizeof(u64), c->stream));
-  r = sync_ctx(c);
-  if (r != DC_SUCCESS) return r;
-  if (root_moves) std::copy(rm.begin(), rm.end(), root_moves);
-  std::vector<u64> div(nr, 0);
-  if (depth == 1) {
-    if (shard == 0)
-      for (u32 i = 0; i < nr; ++i) div[i] = 1;
-  } else {
-    const u32 final_level = depth >= 3 ? depth - 2 : 1;
-    const u32 split = std::max<u32>(1, std::min(split_depth, final_level));
-    u32 level = 1;
-    int buf = 1;
-    auto apply_shard = [&]() {
-      if (n_shards == 1) return;
-      const u64 lo = cur.n * shard / n_shards, hi = cur.n * (shard + 1) / n_shards;
-      cur.nodes += lo;
-      cur.tags += lo;
-      if (cur.meta) cur.meta += lo;
-      cur.n = hi - lo;
-    };
-    while (level < final_level) {
-      if (level == split) apply_shard();
-      if (cur.n == 0) break;
-      r = expand_level(c, rules, pos->stm ^ (level & 1), cur, buf ^ 1, false, &nxt);
-      if (r != DC_SUCCESS) return r;
-      cur = nxt;
-      buf ^= 1;
-      ++level;
-    }
-    if (level == split && level == final_level) apply_shard();
-    const int stm = pos->stm ^ (level & 1);
-    if (cur.n) {
-      if (depth >= 3) {
-        // leaves = grandchildren of the final level
-        HIP_TRY(c->timed("count2", 0, [&] {
-          return rules == DC_RULES_REF
-                     ? dc::launch_count2(c->stream, stm, cur.nodes, cur.tags, (u32)cur.n, c->divide.p, 0)
-                     : dc::launch_count2_fide(c->stream, stm, cur.nodes, cur.meta, cur.tags, (u32)cur.n, c->divide.p, 0);
-        }));
-      } else {
-        HIP_TRY(c->timed("count1", 0, [&] {
-          return rules == DC_RULES_REF
-                     ? dc::launch_count1(c->stream, stm, cur.nodes, cur.tags, (u32)cur.n, c->divide.p)
-                     : dc::launch_count1_fide(c->stream, stm, cur.nodes, cur.meta, cur.tags, (u32)cur.n, c->divide.p);
-        }));
-      }
-    }
-    HIP_TRY(hipMemcpyAsync(div.data(), c->divide.p, nr * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
-    r = sync_ctx(c);
-    if (r != DC_SUCCESS) return r;
-    u64 leaves = 0;
-    for (u32 i = 0; i < nr; ++i) leaves += div[i];
-    if (c->profiling) {
-      auto it = c->stats.find(depth >= 3 ? "count2" : "count1");
-      if (it != c->stats.end()) it->second.units += leaves;
-    }
-  }
+  if (root_moves) std::copy(r.root_moves, r.root_moves + nr, root_moves);
   u64 t = 0;
   for (u32 i = 0; i < nr; ++i) {
-    t += div[i];
-    if (divide) divide[i] = div[i];
+    const u64 v = depth == 1 ? (shard == 0 ? 1 : 0) : r.divide[i];
+    t += v;
+    if (divide) divide[i] = v;
   }
   *total = t;
+  if (c->profiling && depth >= 2) {
+    auto it = c->stats.find(depth >= 3 ? "count2" : "count1");
+    if (it != c->stats.end()) it->second.units += t;
+  }
   return DC_SUCCESS;
 }
 
@@ -736,7 +786,8 @@ int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_p
       ncclGroupStart();
       for (int i = 0; i < n_devices; ++i) {
         (void)hipSetDevice(devices[i]);
-        ncclAllReduce(ctx[i]->divide.p, ctx[i]->divide.p, nroot[0], ncclUint64, ncclSum, comms[i], ctx[i]->stream);
+        ncclAllReduce(ctx[i]->res.p->divide, ctx[i]->res.p->divide, nroot[0], ncclUint64, ncclSum, comms[i],
+                      ctx[i]->stream);
       }
       if (ncclGroupEnd() != ncclSuccess) result = DC_ERCCL;
       for (int i = 0; i < n_devices; ++i) {
@@ -745,7 +796,7 @@ int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_p
       }
       if (result == DC_SUCCESS) {
         (void)hipSetDevice(devices[0]);
-        if (hipMemcpy(div.data(), ctx[0]->divide.p, nroot[0] * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess)
+        if (hipMemcpy(div.data(), ctx[0]->res.p->divide, nroot[0] * sizeof(u64), hipMemcpyDeviceToHost) != hipSuccess)
           result = DC_EHIP;
       }
       for (auto& cm : comms) ncclCommDestroy(cm);

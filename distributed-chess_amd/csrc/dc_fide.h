@@ -14,17 +14,7 @@ hipError_t launch_validate_fide(hipStream_t st, const DevPos* pos, const uint16_
 hipError_t launch_apply_fide(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
                              uint8_t* info);
 hipError_t launch_replay_fide(hipStream_t st, const DevPos& start, const uint16_t* moves, u32 n_games, u32 n_plies,
-                              u64* bitmap, u64* digests, u64* stats);
+                              u64* bitmap, u64* digests, u64* stats, u64* partial);
 hipError_t launch_gen_games_fide(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
                                  uint16_t* out);
-hipError_t launch_count_children_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, u32 n,
-                                      u32* counts);
-hipError_t launch_expand_write_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta,
-                                    const uint16_t* tags, u32 n, const u64* offsets, Board* out, uint16_t* out_meta,
-                                    uint16_t* out_tags, uint16_t* out_moves, int root_level);
-hipError_t launch_count1_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, const uint16_t* tags,
-                              u32 n, u64* divide);
-hipError_t launch_count2_fide(hipStream_t st, int stm, const Board* nodes, const uint16_t* meta, const uint16_t* tags,
-                              u32 n, u64* divide, u32 max_blocks);
-
 }  // namespace dc

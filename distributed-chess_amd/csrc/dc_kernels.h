@@ -40,18 +40,11 @@ __host__ __device__ inline void startpos_board(B& b) {
 hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out);
 hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
                             uint8_t* info);
+// stats[5] = validated, accepted, rejected, digest sum, digest xor; partial has
+// replay_partials(n_games) x 5 u64 of scratch.
+u32 replay_partials(u32 n_games);
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
-                             u32 n_plies, u64* bitmap, u64* digests, u64* stats);
+                             u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial);
 hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
                                 uint16_t* out);
-hipError_t launch_count_children(hipStream_t st, int stm, const Board* nodes, u32 n, u32* counts);
-hipError_t launch_expand_write(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n,
-                               const u64* offsets, Board* out, uint16_t* out_tags, uint16_t* out_moves,
-                               int root_level);
-hipError_t launch_count1(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide);
-hipError_t launch_count2(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, u32 n, u64* divide,
-                         u32 max_blocks);
-size_t scan_temp_elems(u64 n);
-hipError_t launch_scan_u32(hipStream_t st, const u32* in, u64 n, u64* out, u64* temp);
-
 }  // namespace dc

@@ -108,40 +108,39 @@ __device__ __forceinline__ void ref_make(Board& b, int f, int t) {
 }
 
 // validate_move on one (position, move word).  Verdict order chess.rs:82-125.
+// Branch-free: every per-kind rule (chess.rs:214-360) is evaluated as a
+// predicate and the mover's kind selects one, so lanes holding different
+// pieces never serialise on a switch.
 __device__ __forceinline__ u32 ref_verdict(const Board& b, u32 stm, u32 m) {
-  if (m & 0x8000u) return V_OOR;
   const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
   const u32 nib = nibble(b, f);
   const u32 kind = nib >> 1;
-  if (kind == 0) return V_NO_PIECE;
-  if ((nib & 1) != stm) return V_WRONG_TURN;
   const u64 occ = occupied(b);
   const u64 own = stm ? b.b0 : (occ & ~b.b0);
-  const u64 tm = 1ull << t;
+  const u32 t_occ = (u32)(occ >> t) & 1, t_own = (u32)(own >> t) & 1;
   const int dx = (t >> 3) - (f >> 3), dy = (t & 7) - (f & 7);
   const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
-  bool ok;
-  switch (kind) {
-    case KC_P: {
-      const int dir = stm ? -1 : 1;
-      const bool t_empty = (occ & tm) == 0;
-      const bool push = dy == 0 && dx == dir && t_empty;
-      const bool dbl = dy == 0 && dx == 2 * dir && (f >> 3) == (stm ? 6 : 1) && t_empty &&
-                       ((occ >> (f + 8 * dir)) & 1) == 0;
-      const bool cap = ay == 1 && dx == dir && (occ & ~own & tm) != 0;
-      ok = push || dbl || cap;
-      break;
-    }
-    case KC_N: ok = (ax == 1 && ay == 2) || (ax == 2 && ay == 1); break;
-    case KC_K: ok = ax <= 1 && ay <= 1; break;
-    case KC_B: ok = ax == ay && (between(f, t) & occ) == 0; break;
-    case KC_R: ok = (dx == 0 || dy == 0) && (between(f, t) & occ) == 0; break;
-    case KC_Q: ok = (ax == ay || dx == 0 || dy == 0) && (between(f, t) & occ) == 0; break;
-    default: ok = false;  // unknown kind string: can_move_to returns false (chess.rs:210)
-  }
-  // target must be empty or enemy for every kind (pawn rules already imply it)
-  ok = ok && (own & tm) == 0;
-  return ok ? V_OK : V_ILLEGAL;
+  const int dir = stm ? -1 : 1;
+  const u32 mid_occ = (u32)(occ >> ((f + t) >> 1)) & 1;  // only meaningful for a double push
+  const u32 on_start = (u32)((f >> 3) == (stm ? 6 : 1));
+  const u32 push = (u32)(dy == 0) & (u32)(dx == dir) & (t_occ ^ 1);
+  const u32 dbl = (u32)(dy == 0) & (u32)(dx == 2 * dir) & on_start & (t_occ ^ 1) & (mid_occ ^ 1);
+  const u32 cap = (u32)(ay == 1) & (u32)(dx == dir) & t_occ & (t_own ^ 1);
+  const u32 pawn_ok = push | dbl | cap;
+  const u32 knight_ok = (u32)((ax == 1 && ay == 2) || (ax == 2 && ay == 1));
+  const u32 king_ok = (u32)(ax <= 1) & (u32)(ay <= 1);
+  const u32 orth = (u32)(dx == 0) | (u32)(dy == 0);
+  const u32 diag = (u32)(ax == ay);
+  const u32 clear = (u32)((between(f, t) & occ) == 0);
+  // kind codes: P=1 N=2 K=3 X=4 B=5 R=6 Q=7
+  const u32 line_ok = ((kind == KC_B) ? diag : (kind == KC_R) ? orth : (kind == KC_Q) ? (orth | diag) : 0u) & clear;
+  const u32 step_ok = (kind == KC_P) ? pawn_ok : (kind == KC_N) ? knight_ok : (kind == KC_K) ? king_ok : 0u;
+  const u32 ok = (line_ok | step_ok) & (t_own ^ 1);
+  u32 v = ok ? V_OK : V_ILLEGAL;
+  v = ((nib & 1) != stm) ? V_WRONG_TURN : v;
+  v = (kind == 0) ? V_NO_PIECE : v;
+  v = (m & 0x8000u) ? V_OOR : v;
+  return v;
 }
 
 __device__ __forceinline__ u64 board_digest(const Board& b, u32 stm) {
