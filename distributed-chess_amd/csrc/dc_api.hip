@@ -82,8 +82,7 @@ struct dc_ctx {
   DBuf<Board> top_nodes;
   DBuf<uint16_t> top_tags, top_meta;
   DBuf<u32> counts;
-  DBuf<u64> offsets;
-  DBuf<u64> scan_tmp;
+  DBuf<u64> chunk_sum, chunk_base;
   DBuf<dc::PerftResult> res;
   DBuf<dc::Range> rng;
   DBuf<u64> desc;
@@ -104,8 +103,8 @@ struct dc_ctx {
     for (auto* b : {&nodes[0], &nodes[1], &top_nodes, &root}) b->release();
     for (auto* b : {&tags[0], &tags[1], &meta[0], &meta[1], &top_tags, &top_meta, &root_meta, &moves}) b->release();
     counts.release();
-    offsets.release();
-    scan_tmp.release();
+    chunk_sum.release();
+    chunk_base.release();
     res.release();
     rng.release();
     desc.release();
@@ -564,7 +563,6 @@ namespace {
 constexpr u64 kBranchBound = 64;                    // speculative children per node
 constexpr u64 kSpecBudget = 4ull << 30;             // bytes per speculative level
 constexpr u64 kNodeBytes = sizeof(Board) + 2 * sizeof(uint16_t);
-constexpr u64 kDescMaxParents = 1ull << 21;       // final levels up to this size use the descriptor path
 
 int ensure_level(dc_ctx* c, int b, u64 n, bool fide) {
   const size_t want = std::max<u64>(n, 1);
@@ -587,11 +585,12 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
               uint32_t n_shards, bool exact, dc::PerftResult* out) {
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
-  const u32 F = depth >= 3 ? depth - 2 : 1;       // level handed to the final kernel
-  const int final_plies = depth >= 3 ? 2 : 1;     // depth 1: no final kernel
+  const u32 F = depth >= 3 ? depth - 2 : 1;       // level handed to the final stage
+  const int final_plies = depth >= 3 ? 2 : 1;     // depth 1: no final stage
   const u32 S = std::max<u32>(1, std::min(split_depth, F));
-  u32 T = exact ? 1 : std::min<u32>(F, 2);        // levels built by the single-workgroup top kernel
+  u32 T = exact ? 1 : std::min<u32>(F, 3);        // plies built by the single-workgroup top kernel
   if (sharded) T = std::min(T, S);
+  static const u64 kTopCap[4] = {1, 256, 256 * 256, 1ull << 20};
   // buffers (allocated before anything is enqueued)
   if (!c->res_host) HIP_TRY(hipHostMalloc((void**)&c->res_host, sizeof(dc::PerftResult)));
   if (!c->root_host) HIP_TRY(hipHostMalloc((void**)&c->root_host, sizeof(*c->root_host)));
@@ -599,12 +598,20 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
   HIP_TRY(c->rng.ensure(16));
   HIP_TRY(c->root.ensure(1));
   HIP_TRY(c->root_meta.ensure(1));
-  HIP_TRY(c->top_nodes.ensure(256));
-  HIP_TRY(c->top_tags.ensure(256));
-  if (fide) HIP_TRY(c->top_meta.ensure(256));
-  const u64 cap_T = T == 1 ? 256 : 256 * 256;
+  HIP_TRY(c->top_nodes.ensure(kTopCap[1] + kTopCap[2]));
+  HIP_TRY(c->top_tags.ensure(kTopCap[1] + kTopCap[2]));
+  if (fide) HIP_TRY(c->top_meta.ensure(kTopCap[1] + kTopCap[2]));
+  const u64 cap_T = kTopCap[T];
   int e = ensure_level(c, 0, cap_T, fide);
   if (e != DC_SUCCESS) return e;
+  dc::TopScratch ts;
+  for (int k = 0; k < 2; ++k) {
+    const u64 off = k ? kTopCap[1] : 0;
+    ts.nodes[k] = c->top_nodes.p + off;
+    ts.tags[k] = c->top_tags.p + off;
+    ts.meta[k] = fide ? c->top_meta.p + off : nullptr;
+    ts.cap[k] = kTopCap[k + 1];
+  }
   // root upload from pinned memory, result block cleared
   c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
   c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
@@ -612,37 +619,40 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
   HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   HIP_TRY(hipMemsetAsync(c->res.p, 0, sizeof(dc::PerftResult), c->stream));
   HIP_TRY(c->timed("expand_top", 0, [&] {
-    return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, c->top_nodes.p,
-                                 c->top_meta.p, c->top_tags.p, 256, c->nodes[0].p, c->meta[0].p, c->tags[0].p, cap_T,
-                                 c->res.p, c->rng.p + T);
+    return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, ts, c->nodes[0].p,
+                                 fide ? c->meta[0].p : nullptr, c->tags[0].p, cap_T, c->res.p, c->rng.p + T);
   }));
   u32 L = T;
   u64 nb = cap_T;
   int buf = 0;
   if (sharded && L == S) HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
+  // One level: counts + chunk sums, chunk scan into Range L+1 (capacity cap), then `write`.
+  auto count_and_scan = [&](int stm, u64 cap, int select_path) -> int {
+    const u64 nch = std::max<u64>(dc::chunks_for(nb), 1);
+    HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
+    HIP_TRY(c->chunk_sum.ensure(nch));
+    HIP_TRY(c->chunk_base.ensure(nch));
+    HIP_TRY(c->timed("expand_count", 0, [&] {
+      return dc::launch_level_count(c->stream, rules, stm, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
+                                    c->rng.p + L, nb, c->counts.p, c->chunk_sum.p);
+    }));
+    HIP_TRY(c->timed("scan", 0, [&] {
+      return dc::launch_chunk_scan(c->stream, c->chunk_sum.p, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, cap,
+                                   c->res.p, select_path);
+    }));
+    return DC_SUCCESS;
+  };
   while (L < F) {
     const int stm = pos->stm ^ (L & 1);
-    bool exact_level = exact || nb * kBranchBound * kNodeBytes > kSpecBudget;
-    if (exact_level) {
+    if (exact || nb * kBranchBound * kNodeBytes > kSpecBudget) {
       e = read_range(c, L, &nb);
       if (e != DC_SUCCESS) return e;
     }
     u64 cap_next = nb * kBranchBound;
-    HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
-    HIP_TRY(c->offsets.ensure(std::max<u64>(nb, 1)));
-    HIP_TRY(c->scan_tmp.ensure(dc::scan_temp_elems(std::max<u64>(nb, 1))));
-    const Board* in = c->nodes[buf].p;
-    const uint16_t* in_meta = fide ? c->meta[buf].p : nullptr;
-    const uint16_t* in_tags = c->tags[buf].p;
-    HIP_TRY(c->timed("expand_count", 0, [&] {
-      return dc::launch_count_children(c->stream, rules, stm, in, in_meta, c->rng.p + L, nb, c->counts.p);
-    }));
-    exact_level = exact_level && (exact || cap_next * kNodeBytes > kSpecBudget);
-    HIP_TRY(c->timed("scan", 0, [&] {
-      return dc::launch_scan_level(c->stream, c->counts.p, c->rng.p + L, nb, c->offsets.p, c->scan_tmp.p,
-                                   c->rng.p + L + 1, exact_level ? ~0ull : cap_next, c->res.p);
-    }));
-    if (exact_level) {
+    const bool exact_next = exact || cap_next * kNodeBytes > kSpecBudget;
+    e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0);
+    if (e != DC_SUCCESS) return e;
+    if (exact_next) {
       e = read_range(c, L + 1, &cap_next);
       if (e != DC_SUCCESS) return e;
       if (cap_next > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
@@ -650,46 +660,21 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
     e = ensure_level(c, buf ^ 1, cap_next, fide);
     if (e != DC_SUCCESS) return e;
     HIP_TRY(c->timed("expand_write", 0, [&] {
-      return dc::launch_expand_write(c->stream, rules, stm, in, in_meta, in_tags, c->rng.p + L, nb, c->offsets.p,
-                                     c->nodes[buf ^ 1].p, fide ? c->meta[buf ^ 1].p : nullptr, c->tags[buf ^ 1].p,
-                                     cap_next);
+      return dc::launch_level_write(c->stream, rules, stm, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
+                                    c->tags[buf].p, c->rng.p + L, nb, c->counts.p, c->chunk_base.p,
+                                    c->nodes[buf ^ 1].p, fide ? c->meta[buf ^ 1].p : nullptr, c->tags[buf ^ 1].p,
+                                    cap_next);
     }));
     buf ^= 1;
     ++L;
     nb = cap_next;
     if (sharded && L == S) HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
   }
-  const u64 desc_cap = nb * kBranchBound;
-  const bool use_desc = depth >= 3 && !exact && nb <= kDescMaxParents && desc_cap * sizeof(u64) <= kSpecBudget;
-  if (use_desc) {
-    // final level F: children as descriptors (count, scan into Range slot F+1, emit), then one lane per child
-    const int stm = pos->stm ^ (L & 1);
-    const Board* in = c->nodes[buf].p;
-    const uint16_t* in_meta = fide ? c->meta[buf].p : nullptr;
-    HIP_TRY(c->desc.ensure(std::max<u64>(desc_cap, 1)));
-    HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
-    HIP_TRY(c->offsets.ensure(std::max<u64>(nb, 1)));
-    HIP_TRY(c->scan_tmp.ensure(dc::scan_temp_elems(std::max<u64>(nb, 1))));
-    HIP_TRY(c->timed("expand_count", 0, [&] {
-      return dc::launch_count_children(c->stream, rules, stm, in, in_meta, c->rng.p + L, nb, c->counts.p);
-    }));
-    HIP_TRY(c->timed("scan", 0, [&] {
-      return dc::launch_scan_level(c->stream, c->counts.p, c->rng.p + L, nb, c->offsets.p, c->scan_tmp.p,
-                                   c->rng.p + L + 1, desc_cap, c->res.p);
-    }));
-    HIP_TRY(c->timed("emit_desc", 0, [&] {
-      return dc::launch_emit_desc(c->stream, rules, stm, in, in_meta, c->rng.p + L, nb, c->offsets.p, c->desc.p,
-                                  desc_cap);
-    }));
-    HIP_TRY(c->timed("count2", 0, [&] {
-      return dc::launch_count_desc(c->stream, rules, stm, in, in_meta, c->tags[buf].p, c->desc.p, c->rng.p + L + 1,
-                                   desc_cap, c->res.p->divide);
-    }));
-  } else if (depth >= 2) {
-    const int stm = pos->stm ^ (L & 1);
+  const int stm = pos->stm ^ (L & 1);
+  if (depth >= 2) {
     HIP_TRY(c->timed(final_plies == 2 ? "count2" : "count1", 0, [&] {
       return dc::launch_final(c->stream, rules, stm, final_plies, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
-                              c->tags[buf].p, c->rng.p + L, nb, c->res.p->divide);
+                              c->tags[buf].p, c->rng.p + L, nb, c->res.p->divide, nullptr);
     }));
   }
   HIP_TRY(hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream));

@@ -15,30 +15,36 @@ struct PerftResult {
   uint16_t root_moves[256];
   u32 n_root;
   u32 overflow;
+  u32 path;  // final stage: 0 descriptor list, 1 LDS count2
+  u32 pad;
   u64 level_n[16];
 };
 
+// Scratch of the single-workgroup top expansion (plies 1 and 2).
+struct TopScratch {
+  Board* nodes[2];
+  uint16_t* meta[2];
+  uint16_t* tags[2];
+  u64 cap[2];
+};
+
 hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const uint16_t* root_meta, u32 stm0,
-                             u32 target, Board* s_nodes, uint16_t* s_meta, uint16_t* s_tags, u64 cap_s, Board* out,
-                             uint16_t* out_meta, uint16_t* out_tags, u64 cap_out, PerftResult* res, Range* out_rng);
-hipError_t launch_count_children(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                                 const Range* rng, u64 n_bound, u32* counts);
-hipError_t launch_scan_level(hipStream_t st, const u32* counts, const Range* rng, u64 n_bound, u64* offsets, u64* temp,
-                             Range* next, u64 cap_next, PerftResult* res);
-hipError_t launch_expand_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                               const uint16_t* tags, const Range* rng, u64 n_bound, const u64* offsets, Board* out,
-                               uint16_t* out_meta, uint16_t* out_tags, u64 cap);
+                             u32 target, const TopScratch& s, Board* out, uint16_t* out_meta, uint16_t* out_tags,
+                             u64 cap_out, PerftResult* res, Range* out_rng);
+// Per level: count (+ chunk sums), one-workgroup chunk scan (-> next Range), write.
+u64 chunks_for(u64 n);
+hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
+                              const Range* rng, u64 n_bound, u32* counts, u64* chunk_sum);
+hipError_t launch_chunk_scan(hipStream_t st, const u64* chunk_sum, const Range* rng, u64* chunk_base, Range* next,
+                             u64 cap, PerftResult* res, int select_path);
+hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
+                              const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
+                              const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap);
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
-// plies = 1 (k_count1) or 2 (k_count2, the fused last two plies).
+// plies = 1 (k_count1) or 2: the fused last two plies through LDS, k_count2b
+// (256-parent blocks; res == nullptr) or the wave-level k_count2 (runs only
+// when res->path == 1).
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
-                        const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide);
-// The last two plies through an 8-byte child-descriptor list: emit at scanned
-// offsets (count with launch_count_children + launch_scan_level first), then
-// one lane per child; drng = the descriptor list's Range from the scan.
-hipError_t launch_emit_desc(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                            const Range* rng, u64 n_bound, const u64* offsets, u64* desc, u64 cap);
-hipError_t launch_count_desc(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                             const uint16_t* tags, const u64* desc, const Range* drng, u64 n_bound, u64* divide);
-size_t scan_temp_elems(u64 n);
+                        const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res);
 
 }  // namespace dc

@@ -3,21 +3,29 @@
 // A perft(d) run is one fixed launch sequence with the level sizes kept on the
 // device (Range descriptors), so the host synchronises once per run:
 //
-//   k_expand_top      one workgroup expands the root to ply T (<= 2) in LDS-
+//   k_expand_top      one workgroup expands the root to ply T (<= 3) in block-
 //                     scanned, deterministic (parent, class, target) order and
 //                     records the root moves (the divide keys)
-//   k_count_children  K3a  children per frontier node (bulk count)         \  per level,
-//   k_scan_*          exclusive scan -> u64 offsets + next level's Range   |  grid-stride,
-//   k_expand_write    K3b  children written at their offsets (<= cap)      /  n read on device
+//   k_level_count     K3a  children per frontier node (bulk count) + per-chunk  \  3 launches
+//                          sums (a chunk = 256 consecutive nodes = one block)   |  per level,
+//   k_chunk_scan      one workgroup scans the chunk sums -> chunk bases and   |  grid-stride,
+//                     the next level's Range (overflow flagged beyond cap)    |  n read on
+//   k_level_write     K3b  block scan of the chunk + base -> children written   /  the device
 //   k_slice           contiguous shard of a level for data-parallel runs
 //   k_count2          the last two plies fused: per wave, 64 parents' children
 //                     are compacted into LDS (wave prefix sum) and each lane
 //                     makes one child and bulk-counts its moves per round
+//   k_emit_desc +     the last two plies for small parent levels: children as
+//   k_count_desc      8-byte descriptors, then one lane per child (balanced)
 //   k_count1          the last ply alone (depth 2)
 // Writes beyond a level's capacity are dropped and flagged; the host then
 // reruns the exact (host-sized) path.  Divide counts accumulate per root move
 // with one atomic per wave.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <map>
+#include <mutex>
 
 #include "dc_common.h"
 #include "dc_perft.h"
@@ -126,94 +134,180 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
   }
 }
 
-// One workgroup: root (level 0) -> level `target` (1 or 2).  Level 1 lives in
-// scratch; the target level goes to `out` (capacity cap_out) with Range out_rng.
+struct TopBufs {
+  Board* nodes[2];  // scratch for plies 1 and 2 (capacities cap[0], cap[1])
+  uint16_t* meta[2];
+  uint16_t* tags[2];
+  u64 cap[2];
+};
+
+// One workgroup: root (ply 0) -> ply `target` (1..3).  Intermediate plies go
+// to scratch; the target ply goes to `out` (capacity cap_out), Range out_rng.
 template <class R>
-__global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restrict__ root, const uint16_t* __restrict__ root_meta,
-                                                             u32 stm0, u32 target, Board* __restrict__ s_nodes,
-                                                             uint16_t* __restrict__ s_meta, uint16_t* __restrict__ s_tags,
-                                                             u64 cap_s, Board* __restrict__ out, uint16_t* __restrict__ out_meta,
+__global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restrict__ root,
+                                                             const uint16_t* __restrict__ root_meta, u32 stm0,
+                                                             u32 target, TopBufs sb, Board* __restrict__ out,
+                                                             uint16_t* __restrict__ out_meta,
                                                              uint16_t* __restrict__ out_tags, u64 cap_out,
                                                              PerftResult* __restrict__ res, Range* __restrict__ out_rng) {
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
   __shared__ uint16_t s_root_tag;
-  if (threadIdx.x == 0) s_root_tag = 0;
-  __syncthreads();
-  const Board rb = root[0];
-  const uint16_t rmeta = R::kMeta ? root_meta[0] : (uint16_t)0;
-  // level 0 -> 1
-  {
-    Board* dst = target == 1 ? out : s_nodes;
-    uint16_t* dm = target == 1 ? out_meta : s_meta;
-    uint16_t* dt = target == 1 ? out_tags : s_tags;
-    const u64 cap = target == 1 ? cap_out : cap_s;
-    if (stm0) top_level<R, 1>(&rb, &rmeta, &s_root_tag, 1, dst, dm, dt, cap, true, res, wsum, &s_total);
-    else top_level<R, 0>(&rb, &rmeta, &s_root_tag, 1, dst, dm, dt, cap, true, res, wsum, &s_total);
-    __syncthreads();
-    const u64 n1 = s_total;
-    if (threadIdx.x == 0) {
-      res->n_root = (u32)min(n1, (u64)0xFFFFFFFFu);
-      res->level_n[1] = n1;
-      if (n1 > cap || n1 > 256) res->overflow = 1;
-    }
-    if (n1 > cap || n1 > 256) {
-      if (threadIdx.x == 0) *out_rng = Range{0, 0};
-      return;
-    }
-    if (target == 1) {
-      if (threadIdx.x == 0) *out_rng = Range{0, n1};
-      return;
-    }
-  }
-  // level 1 -> 2
-  __syncthreads();
-  const u64 n1 = s_total;
-  __syncthreads();
-  if (stm0) top_level<R, 0>(s_nodes, s_meta, s_tags, n1, out, out_meta, out_tags, cap_out, false, res, wsum, &s_total);
-  else top_level<R, 1>(s_nodes, s_meta, s_tags, n1, out, out_meta, out_tags, cap_out, false, res, wsum, &s_total);
-  __syncthreads();
+  __shared__ Board s_root;
+  __shared__ uint16_t s_root_meta;
   if (threadIdx.x == 0) {
-    const u64 n2 = s_total;
-    res->level_n[2] = n2;
-    if (n2 > cap_out) {
-      res->overflow = 1;
-      *out_rng = Range{0, 0};
-    } else {
-      *out_rng = Range{0, n2};
-    }
+    s_root_tag = 0;
+    s_root = root[0];
+    s_root_meta = R::kMeta ? root_meta[0] : (uint16_t)0;
   }
+  __syncthreads();
+  const Board* cur = &s_root;
+  const uint16_t* cur_meta = &s_root_meta;
+  const uint16_t* cur_tags = &s_root_tag;
+  u64 n = 1;
+  for (u32 ply = 1; ply <= target; ++ply) {
+    const bool last = ply == target;
+    Board* dst = last ? out : sb.nodes[ply - 1];
+    uint16_t* dm = last ? out_meta : sb.meta[ply - 1];
+    uint16_t* dt = last ? out_tags : sb.tags[ply - 1];
+    const u64 cap = last ? cap_out : sb.cap[ply - 1];
+    if ((stm0 ^ (ply - 1)) & 1) top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total);
+    else top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total);
+    __syncthreads();
+    n = s_total;
+    __syncthreads();
+    bool bad = n > cap;
+    if (ply == 1) {
+      bad = bad || n > 256;
+      if (threadIdx.x == 0) res->n_root = (u32)min(n, (u64)0xFFFFFFFFu);
+    }
+    if (threadIdx.x == 0) res->level_n[ply] = n;
+    if (bad) {
+      if (threadIdx.x == 0) {
+        res->overflow = 1;
+        *out_rng = Range{0, 0};
+      }
+      return;
+    }
+    cur = dst;
+    cur_meta = dm;
+    cur_tags = dt;
+  }
+  if (threadIdx.x == 0) *out_rng = Range{0, n};
 }
 
 // ---------------------------------------------------------- level kernels
+// A chunk is 256 consecutive nodes of the level's range, processed by one
+// block; chunk sums are scanned by one workgroup; no global atomics.
+constexpr u32 kChunk = 256;
+
 template <class R, int STM>
-__global__ __launch_bounds__(256) void k_count_children(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
-                                                        const Range* __restrict__ rng, u32* __restrict__ counts) {
+__global__ __launch_bounds__(256) void k_level_count(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                     const Range* __restrict__ rng, u32* __restrict__ counts,
+                                                     u64* __restrict__ chunk_sum) {
+  __shared__ u64 wsum[4];
   const u64 lo = rng->lo, hi = rng->hi;
-  for (u64 i = lo + (u64)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (u64)gridDim.x * blockDim.x)
-    counts[i - lo] = R::template count<STM>(load_board(nodes, i), load_meta<R>(meta, i));
+  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
+  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
+    const u64 i = lo + c * kChunk + threadIdx.x;
+    u32 cnt = 0;
+    if (i < hi) {
+      cnt = R::template count<STM>(load_board(nodes, i), load_meta<R>(meta, i));
+      counts[i - lo] = cnt;
+    }
+    u64 tot;
+    block_excl_scan64<4>(cnt, wsum, &tot);
+    if (threadIdx.x == 0) chunk_sum[c] = tot;
+  }
+}
+
+// Exclusive scan of the chunk sums of `rng` (one 1024-thread workgroup); writes
+// the next level's Range and flags overflow beyond cap.
+// select_path != 0: instead of flagging overflow, a total beyond cap -- or a
+// parent level larger than select_path nodes -- selects the LDS count2 path
+// (res->path = 1) and leaves the descriptor range empty.
+__global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restrict__ chunk_sum, const Range* __restrict__ rng,
+                                                             u64* __restrict__ chunk_base, Range* __restrict__ next,
+                                                             u64 cap, PerftResult* __restrict__ res, int select_path) {
+  __shared__ u64 wsum[kTopThreads / 64];
+  const u64 nch = (rng->hi - rng->lo + kChunk - 1) / kChunk;
+  const u64 per = (nch + kTopThreads - 1) / kTopThreads;
+  const u64 a = min(nch, (u64)threadIdx.x * per), b = min(nch, a + per);
+  u64 s = 0;
+  for (u64 c = a; c < b; ++c) s += chunk_sum[c];
+  u64 total;
+  u64 run = block_excl_scan64<kTopThreads / 64>(s, wsum, &total);
+  for (u64 c = a; c < b; ++c) {
+    const u64 v = chunk_sum[c];
+    chunk_base[c] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) {
+    // large parent levels keep count2 busy on their own: no descriptor round trip
+    if (select_path && rng->hi - rng->lo > (u64)select_path) total = cap + 1;
+    if (total > cap) {  // the level would not fit: flag it (or pick count2) and leave the range empty
+      if (select_path) res->path = 1;
+      else res->overflow = 1;
+      *next = Range{0, 0};
+    } else {
+      *next = Range{0, total};
+    }
+  }
 }
 
 template <class R, int STM>
-__global__ __launch_bounds__(256) void k_expand_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
-                                                      const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
-                                                      const u64* __restrict__ offsets, Board* __restrict__ out,
-                                                      uint16_t* __restrict__ out_meta, uint16_t* __restrict__ out_tags,
-                                                      u64 cap) {
+__global__ __launch_bounds__(256) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
+                                                     const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
+                                                     Board* __restrict__ out, uint16_t* __restrict__ out_meta,
+                                                     uint16_t* __restrict__ out_tags, u64 cap) {
+  __shared__ u64 wsum[4];
   const u64 lo = rng->lo, hi = rng->hi;
-  for (u64 i = lo + (u64)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (u64)gridDim.x * blockDim.x) {
+  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
+  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
+    const u64 i = lo + c * kChunk + threadIdx.x;
+    const bool valid = i < hi;
+    const u32 cnt = valid ? counts[i - lo] : 0;
+    u64 tot;
+    u64 o = block_excl_scan64<4>(cnt, wsum, &tot) + chunk_base[c];
+    if (!valid) continue;
     const Board p = load_board(nodes, i);
     const u32 pm = load_meta<R>(meta, i);
     const uint16_t tag = tags[i];
-    u64 o = offsets[i - lo];
     R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
       if (o < cap) {
-        Board c = p;
-        const u32 cm = R::template make<STM>(c, pm, f, t, promo);
-        store_board(out, o, c);
+        Board ch = p;
+        const u32 cm = R::template make<STM>(ch, pm, f, t, promo);
+        store_board(out, o, ch);
         if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
         out_tags[o] = tag;
       }
+      ++o;
+    });
+  }
+}
+
+// Children of the final level as 8-byte descriptors {parent index, move}.
+template <class R, int STM>
+__global__ __launch_bounds__(256) void k_emit_desc(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                   const Range* __restrict__ rng, const u32* __restrict__ counts,
+                                                   const u64* __restrict__ chunk_base, u64* __restrict__ desc, u64 cap,
+                                                   const PerftResult* __restrict__ res) {
+  __shared__ u64 wsum[4];
+  if (res->path != 0) return;  // count2 was selected
+  const u64 lo = rng->lo, hi = rng->hi;
+  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
+  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
+    const u64 i = lo + c * kChunk + threadIdx.x;
+    const bool valid = i < hi;
+    const u32 cnt = valid ? counts[i - lo] : 0;
+    u64 tot;
+    u64 o = block_excl_scan64<4>(cnt, wsum, &tot) + chunk_base[c];
+    if (!valid) continue;
+    const Board p = load_board(nodes, i);
+    const u32 pm = load_meta<R>(meta, i);
+    R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
+      if (o < cap) desc[o] = i | ((u64)((u32)f | ((u32)t << 6) | ((u32)promo << 12)) << 32);
       ++o;
     });
   }
@@ -257,7 +351,8 @@ struct C2Shared {
 template <class R, int STM>
 __global__ __launch_bounds__(256, 4) void k_count2(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                 const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
-                                                u64* __restrict__ divide) {
+                                                u64* __restrict__ divide, const PerftResult* __restrict__ res) {
+  if (res && res->path == 0) return;  // the descriptor path was selected
   __shared__ C2Shared sh;
   tag_hist_init(sh.hist);
   const u32 w = threadIdx.x >> 6;
@@ -319,151 +414,172 @@ __global__ __launch_bounds__(256, 4) void k_count2(const Board* __restrict__ nod
   tag_hist_flush(sh.hist, divide);
 }
 
-// ------------------------------------------------- descriptor path (small final levels)
-// k_emit_desc: the parents' children become 8-byte descriptors {parent index,
-// move} at scanned offsets (k_count_children + scan, no atomics).  k_count_desc
-// then gives every child its own lane, so the last ply is balanced over the
-// whole GPU even when the parent level is too small to fill it in wave-sized
-// groups.
+// ---------------------------------------------------- k_count2b (final stage)
+// The last two plies, one block = 256 parents (one per lane).  Their children
+// (from, to, promo, parent) are compacted into LDS at block-scan offsets, then
+// all 256 lanes take one child per round: make it, bulk-count its moves.  The
+// work unit is a 256-parent chunk, so even a ~200k-node final level (perft 6)
+// spreads evenly over the GPU, and no child ever round-trips through HBM.
+constexpr u32 kC2bCap = 256 * 28;  // child slots per window (4 blocks per CU)
+
+struct C2bShared {
+  Board par[256];
+  u32 pmeta[256];
+  u32 slot[kC2bCap];
+  u64 hist[256];
+  u64 wsum[4];
+  uint16_t ptag[256];
+};
+
 template <class R, int STM>
-__global__ __launch_bounds__(256) void k_emit_desc(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
-                                                   const Range* __restrict__ rng, const u64* __restrict__ offsets,
-                                                   u64* __restrict__ desc, u64 cap) {
+__global__ __launch_bounds__(256, 4) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                    const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
+                                                    u64* __restrict__ divide) {
+  __shared__ C2bShared sh;
+  tag_hist_init(sh.hist);
+  const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
-  for (u64 i = lo + (u64)blockIdx.x * blockDim.x + threadIdx.x; i < hi; i += (u64)gridDim.x * blockDim.x) {
-    const Board p = load_board(nodes, i);
-    const u32 pm = load_meta<R>(meta, i);
-    u64 o = offsets[i - lo];
-    R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
-      if (o < cap) desc[o] = i | ((u64)((u32)f | ((u32)t << 6) | ((u32)promo << 12)) << 32);
-      ++o;
-    });
-  }
-}
-
-template <class R, int STM>
-__global__ __launch_bounds__(256) void k_count_desc(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
-                                                    const uint16_t* __restrict__ tags, const u64* __restrict__ desc,
-                                                    const Range* __restrict__ drng, u64* __restrict__ divide) {
-  __shared__ u64 hist[256];
-  tag_hist_init(hist);
-  const u64 n = drng->hi;
-  for (u64 base = (u64)blockIdx.x * blockDim.x; base < n; base += (u64)gridDim.x * blockDim.x) {
-    const u64 j = base + threadIdx.x;
-    const bool valid = j < n;
-    u32 k = 0, tag = 0;
+  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
+  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
+    const u64 i = lo + c * kChunk + tid;
+    const bool valid = i < hi;
+    Board p{0, 0, 0, 0};
+    u32 pm = 0, tag = 0;
     if (valid) {
-      const u64 d = desc[j];
-      const u64 pi = d & 0xFFFFFFFFull;
-      const u32 m = (u32)(d >> 32);
-      Board c = load_board(nodes, pi);
-      const u32 cm = R::template make<STM>(c, load_meta<R>(meta, pi), (int)(m & 63), (int)((m >> 6) & 63),
-                                           (int)((m >> 12) & 7));
-      k = R::template count<1 - STM>(c, cm);
-      tag = tags[pi];
+      p = load_board(nodes, i);
+      pm = load_meta<R>(meta, i);
+      tag = tags[i];
     }
-    tag_hist_add(hist, tag, k, valid);
-  }
-  tag_hist_flush(hist, divide);
-}
-
-// -------------------------------------------------------------------- scan
-constexpr int kScanItems = 16;
-constexpr int kScanBlock = 256 * kScanItems;
-
-// n: explicit (n_dev == nullptr) or rng->hi - rng->lo.
-template <class T>
-__global__ __launch_bounds__(256) void k_scan_reduce(const T* __restrict__ in, u64 n_static, const Range* __restrict__ rng,
-                                                     u64* __restrict__ bsums) {
-  __shared__ u64 wsum[4];
-  const u64 n = rng ? rng->hi - rng->lo : n_static;
-  const u64 base = (u64)blockIdx.x * kScanBlock + (u64)threadIdx.x * kScanItems;
-  u64 s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k)
-    if (base + k < n) s += in[base + k];
-  u64 tot;
-  block_excl_scan64<4>(s, wsum, &tot);
-  if (threadIdx.x == 0) bsums[blockIdx.x] = tot;
-}
-
-// Writes exclusive offsets; with `next` set, the thread holding the last
-// element publishes the next level's Range and flags overflow beyond `cap`.
-template <class T>
-__global__ __launch_bounds__(256) void k_scan_apply(const T* __restrict__ in, u64 n_static, const Range* __restrict__ rng,
-                                                    const u64* __restrict__ bexcl, u64* __restrict__ out,
-                                                    Range* __restrict__ next, u64 cap, PerftResult* __restrict__ res) {
-  __shared__ u64 wsum[4];
-  const u64 n = rng ? rng->hi - rng->lo : n_static;
-  const u64 base = (u64)blockIdx.x * kScanBlock + (u64)threadIdx.x * kScanItems;
-  T vals[kScanItems];
-  u64 s = 0;
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    vals[k] = (base + k < n) ? in[base + k] : (T)0;
-    s += vals[k];
-  }
-  u64 tot;
-  u64 run = block_excl_scan64<4>(s, wsum, &tot) + (bexcl ? bexcl[blockIdx.x] : 0);
-#pragma unroll
-  for (int k = 0; k < kScanItems; ++k) {
-    if (base + k < n) {
-      out[base + k] = run;
-      if (next && base + k == n - 1) {
-        const u64 total = run + vals[k];
-        if (total > cap) {  // the level did not fit: flag it and leave the rest of the run empty
-          res->overflow = 1;
-          *next = Range{0, 0};
-        } else {
-          *next = Range{0, total};
+    const u32 cnt = valid ? R::template count<STM>(p, pm) : 0;
+    u64 total64;
+    const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
+    const u32 total = (u32)total64;
+    sh.par[tid] = p;
+    if constexpr (R::kMeta) sh.pmeta[tid] = pm;
+    sh.ptag[tid] = (uint16_t)tag;
+    __syncthreads();
+    const u32 tag0 = sh.ptag[0];
+    u64 acc = 0;  // grandchildren under parents whose tag == tag0 (the norm: nodes stay ordered by root)
+    for (u32 base = 0; base < total; base += kC2bCap) {
+      if (base) __syncthreads();  // previous window fully read
+      u32 j = excl;
+      if (valid && j < base + kC2bCap && j + cnt > base) {
+        R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
+          if (j >= base && j - base < kC2bCap) sh.slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (tid << 15);
+          ++j;
+        });
+      }
+      __syncthreads();
+      const u32 nslots = min(kC2bCap, total - base);
+      for (u32 r0 = 0; r0 < nslots; r0 += 256) {
+        const u32 r = r0 + tid;
+        if (r < nslots) {
+          const u32 e = sh.slot[r];
+          const u32 pl = e >> 15;
+          Board ch = sh.par[pl];
+          const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
+                                               (int)((e >> 12) & 7));
+          const u32 k = R::template count<1 - STM>(ch, cm);
+          const u32 ptag = sh.ptag[pl];
+          if (ptag == tag0) acc += k;
+          else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
         }
       }
     }
-    run += vals[k];
+    tag_hist_add(sh.hist, tag0, acc, true);
+    __syncthreads();  // par/ptag/slot reused by the next chunk
   }
-  if (next && n == 0 && blockIdx.x == 0 && threadIdx.x == 0) *next = Range{0, 0};
+  tag_hist_flush(sh.hist, divide);
 }
 
 // ------------------------------------------------------------- launchers
-static constexpr u32 kMaxGrid = 2048;  // 8 blocks of 256 per CU; grid-stride beyond
+static constexpr u32 kMaxGrid = 1u << 20;
 
 static inline u32 grid_for(u64 n, u32 per) {
   const u64 b = (n + per - 1) / per;
   return (u32)std::max<u64>(1, std::min<u64>(b, kMaxGrid));
 }
 
-#define DC_LAUNCH_STM(KERNEL, R, grid, block, st, ...)                                           \
+// Grid-stride kernels get at most one resident wave of blocks (occupancy x CUs):
+// a second, partial round of statically assigned blocks is pure tail.
+template <class K>
+static u32 resident_grid(K kernel, u32 block, u32 want) {
+  static std::mutex mu;
+  static std::map<const void*, u32> cache;
+  const void* key = reinterpret_cast<const void*>(kernel);
+  u32 cap;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    auto it = cache.find(key);
+    if (it == cache.end()) {
+      int per_cu = 0, dev = 0, cus = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, (int)block, 0) != hipSuccess || per_cu < 1)
+        per_cu = 1;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 256;
+      it = cache.emplace(key, (u32)(per_cu * cus)).first;
+    }
+    cap = it->second;
+  }
+  return std::max<u32>(1, std::min(want, cap));
+}
+
+#define DC_LAUNCH_STM(KERNEL, R, grid, block, st, ...)                                                     \
+  do {                                                                                                     \
+    if (stm) {                                                                                             \
+      auto k_ = KERNEL<R, 1>;                                                                              \
+      hipLaunchKernelGGL(k_, dim3(resident_grid(k_, block, grid)), dim3(block), 0, st, __VA_ARGS__);      \
+    } else {                                                                                               \
+      auto k_ = KERNEL<R, 0>;                                                                              \
+      hipLaunchKernelGGL(k_, dim3(resident_grid(k_, block, grid)), dim3(block), 0, st, __VA_ARGS__);      \
+    }                                                                                                      \
+  } while (0)
+
+#define DC_LAUNCH_RULES_STM(KERNEL, grid, block, st, ...)                                        \
   do {                                                                                           \
-    if (stm) hipLaunchKernelGGL((KERNEL<R, 1>), dim3(grid), dim3(block), 0, st, __VA_ARGS__);   \
-    else hipLaunchKernelGGL((KERNEL<R, 0>), dim3(grid), dim3(block), 0, st, __VA_ARGS__);       \
+    if (rules == 0) DC_LAUNCH_STM(KERNEL, RefRules, grid, block, st, __VA_ARGS__);              \
+    else DC_LAUNCH_STM(KERNEL, FideRules, grid, block, st, __VA_ARGS__);                        \
   } while (0)
 
 hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const uint16_t* root_meta, u32 stm0,
-                             u32 target, Board* s_nodes, uint16_t* s_meta, uint16_t* s_tags, u64 cap_s, Board* out,
-                             uint16_t* out_meta, uint16_t* out_tags, u64 cap_out, PerftResult* res, Range* out_rng) {
+                             u32 target, const TopScratch& s, Board* out, uint16_t* out_meta, uint16_t* out_tags,
+                             u64 cap_out, PerftResult* res, Range* out_rng) {
+  TopBufs b;
+  for (int k = 0; k < 2; ++k) {
+    b.nodes[k] = s.nodes[k];
+    b.meta[k] = s.meta[k];
+    b.tags[k] = s.tags[k];
+    b.cap[k] = s.cap[k];
+  }
   if (rules == 0)
-    hipLaunchKernelGGL(k_expand_top<RefRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, s_nodes,
-                       s_meta, s_tags, cap_s, out, out_meta, out_tags, cap_out, res, out_rng);
+    hipLaunchKernelGGL(k_expand_top<RefRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, b, out,
+                       out_meta, out_tags, cap_out, res, out_rng);
   else
-    hipLaunchKernelGGL(k_expand_top<FideRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target,
-                       s_nodes, s_meta, s_tags, cap_s, out, out_meta, out_tags, cap_out, res, out_rng);
+    hipLaunchKernelGGL(k_expand_top<FideRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, b,
+                       out, out_meta, out_tags, cap_out, res, out_rng);
   return hipGetLastError();
 }
 
-hipError_t launch_count_children(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                                 const Range* rng, u64 n_bound, u32* counts) {
-  const u32 g = grid_for(n_bound, 256);
-  if (rules == 0) DC_LAUNCH_STM(k_count_children, RefRules, g, 256, st, nodes, meta, rng, counts);
-  else DC_LAUNCH_STM(k_count_children, FideRules, g, 256, st, nodes, meta, rng, counts);
+u64 chunks_for(u64 n) { return (n + kChunk - 1) / kChunk; }
+
+hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
+                              const Range* rng, u64 n_bound, u32* counts, u64* chunk_sum) {
+  DC_LAUNCH_RULES_STM(k_level_count, grid_for(n_bound, kChunk), 256, st, nodes, meta, rng, counts, chunk_sum);
   return hipGetLastError();
 }
 
-hipError_t launch_expand_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                               const uint16_t* tags, const Range* rng, u64 n_bound, const u64* offsets, Board* out,
-                               uint16_t* out_meta, uint16_t* out_tags, u64 cap) {
-  const u32 g = grid_for(n_bound, 256);
-  if (rules == 0) DC_LAUNCH_STM(k_expand_write, RefRules, g, 256, st, nodes, meta, tags, rng, offsets, out, out_meta, out_tags, cap);
-  else DC_LAUNCH_STM(k_expand_write, FideRules, g, 256, st, nodes, meta, tags, rng, offsets, out, out_meta, out_tags, cap);
+hipError_t launch_chunk_scan(hipStream_t st, const u64* chunk_sum, const Range* rng, u64* chunk_base, Range* next,
+                             u64 cap, PerftResult* res, int select_path) {
+  hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(kTopThreads), 0, st, chunk_sum, rng, chunk_base, next, cap, res,
+                     select_path);
+  return hipGetLastError();
+}
+
+hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
+                              const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
+                              const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap) {
+  DC_LAUNCH_RULES_STM(k_level_write, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, counts, chunk_base,
+                      out, out_meta, out_tags, cap);
   return hipGetLastError();
 }
 
@@ -473,77 +589,10 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
 }
 
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
-                        const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide) {
-  if (plies == 1) {
-    const u32 g = grid_for(n_bound, 256);
-    if (rules == 0) DC_LAUNCH_STM(k_count1, RefRules, g, 256, st, nodes, meta, tags, rng, divide);
-    else DC_LAUNCH_STM(k_count1, FideRules, g, 256, st, nodes, meta, tags, rng, divide);
-  } else {
-    const u32 g = grid_for(n_bound, 64 * kC2Waves);
-    if (rules == 0) DC_LAUNCH_STM(k_count2, RefRules, g, 256, st, nodes, meta, tags, rng, divide);
-    else DC_LAUNCH_STM(k_count2, FideRules, g, 256, st, nodes, meta, tags, rng, divide);
-  }
-  return hipGetLastError();
-}
-
-hipError_t launch_emit_desc(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                            const Range* rng, u64 n_bound, const u64* offsets, u64* desc, u64 cap) {
-  const u32 g = grid_for(n_bound, 256);
-  if (rules == 0) DC_LAUNCH_STM(k_emit_desc, RefRules, g, 256, st, nodes, meta, rng, offsets, desc, cap);
-  else DC_LAUNCH_STM(k_emit_desc, FideRules, g, 256, st, nodes, meta, rng, offsets, desc, cap);
-  return hipGetLastError();
-}
-
-hipError_t launch_count_desc(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
-                             const uint16_t* tags, const u64* desc, const Range* drng, u64 n_bound, u64* divide) {
-  const u32 g = grid_for(n_bound, 256);
-  if (rules == 0) DC_LAUNCH_STM(k_count_desc, RefRules, g, 256, st, nodes, meta, tags, desc, drng, divide);
-  else DC_LAUNCH_STM(k_count_desc, FideRules, g, 256, st, nodes, meta, tags, desc, drng, divide);
-  return hipGetLastError();
-}
-
-size_t scan_temp_elems(u64 n) {
-  size_t tot = 0;
-  while (n > 1) {
-    n = (n + kScanBlock - 1) / kScanBlock;
-    tot += 2 * n;
-  }
-  return tot + 2;
-}
-
-// Recursive scan of static-size u64 block sums.
-static hipError_t scan_static(hipStream_t st, const u64* in, u64 n, u64* out, u64* temp) {
-  const u32 nb = (u32)((n + kScanBlock - 1) / kScanBlock);
-  if (nb <= 1) {
-    hipLaunchKernelGGL(k_scan_apply<u64>, dim3(1), dim3(256), 0, st, in, n, (const Range*)nullptr, (const u64*)nullptr,
-                       out, (Range*)nullptr, (u64)0, (PerftResult*)nullptr);
-    return hipGetLastError();
-  }
-  u64* bsums = temp;
-  u64* bexcl = temp + nb;
-  hipLaunchKernelGGL(k_scan_reduce<u64>, dim3(nb), dim3(256), 0, st, in, n, (const Range*)nullptr, bsums);
-  hipError_t e = scan_static(st, bsums, nb, bexcl, temp + 2 * (size_t)nb);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_scan_apply<u64>, dim3(nb), dim3(256), 0, st, in, n, (const Range*)nullptr, bexcl, out,
-                     (Range*)nullptr, (u64)0, (PerftResult*)nullptr);
-  return hipGetLastError();
-}
-
-hipError_t launch_scan_level(hipStream_t st, const u32* counts, const Range* rng, u64 n_bound, u64* offsets, u64* temp,
-                             Range* next, u64 cap_next, PerftResult* res) {
-  const u32 nb = (u32)std::max<u64>(1, (n_bound + kScanBlock - 1) / kScanBlock);
-  if (nb == 1) {
-    hipLaunchKernelGGL(k_scan_apply<u32>, dim3(1), dim3(256), 0, st, counts, (u64)0, rng, (const u64*)nullptr, offsets,
-                       next, cap_next, res);
-    return hipGetLastError();
-  }
-  u64* bsums = temp;
-  u64* bexcl = temp + nb;
-  hipLaunchKernelGGL(k_scan_reduce<u32>, dim3(nb), dim3(256), 0, st, counts, (u64)0, rng, bsums);
-  hipError_t e = scan_static(st, bsums, nb, bexcl, temp + 2 * (size_t)nb);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_scan_apply<u32>, dim3(nb), dim3(256), 0, st, counts, (u64)0, rng, bexcl, offsets, next, cap_next,
-                     res);
+                        const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res) {
+  if (plies == 1) DC_LAUNCH_RULES_STM(k_count1, grid_for(n_bound, 256), 256, st, nodes, meta, tags, rng, divide);
+  else if (res == nullptr) DC_LAUNCH_RULES_STM(k_count2b, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, divide);
+  else DC_LAUNCH_RULES_STM(k_count2, grid_for(n_bound, 64 * kC2Waves), 256, st, nodes, meta, tags, rng, divide, res);
   return hipGetLastError();
 }
 
