@@ -144,8 +144,7 @@ def main():
         tot, _, _ = perft_step(eng, d, args, pos)
         if want is not None and tot != want:
             raise SystemExit(f"parity failure: perft({args.depth}) = {tot}, expected {want}")
-    eng.reset_stats()
-    eng.set_profiling(True)
+    # timed region: no per-launch events (they add ~40 us of host work per step)
     d.sync()
     t0 = time.perf_counter()
     leaves = 0
@@ -154,12 +153,21 @@ def main():
         leaves += tot
     d.sync()
     dt = d.max(time.perf_counter() - t0)
-    eng.set_profiling(False)
     if want is not None and leaves != want * args.steps:
         raise SystemExit(f"parity failure in timed region: {leaves} != {want} x {args.steps}")
+    # kernel durations: the same steps again with HIP events around every launch
+    # on the context's stream (dc_ctx_set_profiling), for the roofline
+    eng.reset_stats()
+    eng.set_profiling(True)
+    for _ in range(args.steps):
+        perft_step(eng, d, args, pos)
+    d.sync()
+    eng.set_profiling(False)
     c2 = eng.kernel_stats("count2")
     exp_c = eng.kernel_stats("expand_count")
     exp_w = eng.kernel_stats("expand_write")
+    top = eng.kernel_stats("expand_top")
+    scan = eng.kernel_stats("scan")
 
     # --------------------------------------------------------------- replay
     replay = None
@@ -170,8 +178,6 @@ def main():
         d_dg = eng.alloc(n * 8)
         eng.gen_games_device(d_moves, 0x5EED20241022, d.rank * n, n, plies, 32)  # inputs resident before timing
         st = eng.replay_device(d_moves, n, plies, d_bm, d_dg)
-        eng.reset_stats()
-        eng.set_profiling(True)
         d.sync()
         t0 = time.perf_counter()
         validated = 0
@@ -180,6 +186,10 @@ def main():
             validated += st["validated"]
         d.sync()
         rdt = d.max(time.perf_counter() - t0)
+        eng.reset_stats()
+        eng.set_profiling(True)
+        for _ in range(args.replay_steps):
+            eng.replay_device(d_moves, n, plies, d_bm, d_dg)
         eng.set_profiling(False)
         rk = eng.kernel_stats("replay")
         tot_validated = int(d.allreduce_u64(np.array([validated], np.uint64))[0])
@@ -219,8 +229,9 @@ def main():
                                f"frontier split at ply {args.split} over ranks", "depth": args.depth,
                    "rules": "REF", "leaves_per_step": want, "parallelism": f"dp{d.world}"},
         "roofline": roof,
-        "kernels": {"count2_ms_per_step": c2["total_ms"] / args.steps,
-                    "expand_ms_per_step": (exp_c["total_ms"] + exp_w["total_ms"]) / args.steps},
+        "kernels_ms_per_step": {k: v["total_ms"] / args.steps for k, v in
+                                (("expand_top", top), ("expand_count", exp_c), ("scan", scan),
+                                 ("expand_write", exp_w), ("count2", c2))},
     }
     if replay is not None:
         line["replay"] = replay

@@ -26,14 +26,34 @@ constexpr u64 kAll = ~0ull;
 constexpr u64 kDiagMain = 0x8040201008040201ull;  // a1..h8 (x - y == 0)
 constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
 
-// Generalised shift: S > 0 toward higher squares.
+// Generalised shift: S > 0 toward higher squares.  Emitted as one
+// v_lshlrev_b64 / v_lshrrev_b64: on gfx950 every shift issues at half rate,
+// so one 64-bit shift (4 cycles per wave) beats the compiler's habit of
+// splitting it into v_alignbit_b32 + v_lshlrev_b32 once the halves feed
+// 32-bit bitop3s (tools/ubench/vop_rate.hip, profiles/r01/ubench_vop.txt).
 template <int S>
 __device__ __forceinline__ u64 sh(u64 x) {
-  if constexpr (S >= 0) return x << S;
-  else return x >> (-S);
+  u64 r;
+  if constexpr (S > 0) asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
+  else if constexpr (S < 0) asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(-S), "v"(x));
+  else r = x;
+  return r;
 }
 
 __device__ __forceinline__ u32 pc(u64 x) { return (u32)__popcll(x); }
+
+// gfx950 v_bitop3_b32: any 3-input bitwise function in one full-rate
+// instruction per 32-bit half (v_and_or_b32 is half rate).  IMM is the truth
+// table f(0xF0, 0xCC, 0xAA).
+template <unsigned IMM>
+__device__ __forceinline__ u64 bop3(u64 a, u64 b, u64 c) {
+  const u32 lo = __builtin_amdgcn_bitop3_b32((u32)a, (u32)b, (u32)c, IMM);
+  const u32 hi = __builtin_amdgcn_bitop3_b32((u32)(a >> 32), (u32)(b >> 32), (u32)(c >> 32), IMM);
+  return ((u64)hi << 32) | lo;
+}
+__device__ __forceinline__ u64 and3(u64 a, u64 b, u64 c) { return bop3<0x80>(a, b, c); }     // a & b & c
+__device__ __forceinline__ u64 or_and(u64 a, u64 b, u64 c) { return bop3<0xF8>(a, b, c); }   // a | (b & c)
+__device__ __forceinline__ u64 and_andn(u64 a, u64 b, u64 c) { return bop3<0x40>(a, b, c); } // a & b & ~c
 __device__ __forceinline__ int lsb(u64 x) { return __ffsll((long long)x) - 1; }
 __device__ __forceinline__ int msb(u64 x) { return 63 - __clzll((long long)x); }
 
@@ -44,12 +64,24 @@ __device__ __forceinline__ int msb(u64 x) { return 63 - __clzll((long long)x); }
 template <int S, u64 M>
 __device__ __forceinline__ u64 ray_attacks(u64 gen, u64 empty) {
   u64 pro = empty & M;
-  gen |= pro & sh<S>(gen);
+  gen = or_and(gen, pro, sh<S>(gen));
   pro &= sh<S>(pro);
-  gen |= pro & sh<2 * S>(gen);
+  gen = or_and(gen, pro, sh<2 * S>(gen));
   pro &= sh<2 * S>(pro);
-  gen |= pro & sh<4 * S>(gen);
+  gen = or_and(gen, pro, sh<4 * S>(gen));
   return sh<S>(gen) & M;
+}
+
+// Same fill, returning the attacks already masked by `allowed` (one bitop3).
+template <int S, u64 M>
+__device__ __forceinline__ u64 ray_moves(u64 gen, u64 empty, u64 allowed) {
+  u64 pro = empty & M;
+  gen = or_and(gen, pro, sh<S>(gen));
+  pro &= sh<S>(pro);
+  gen = or_and(gen, pro, sh<2 * S>(gen));
+  pro &= sh<2 * S>(pro);
+  gen = or_and(gen, pro, sh<4 * S>(gen));
+  return and3(sh<S>(gen), M, allowed);
 }
 
 // The squares of the line through t in direction class D, strictly on the

@@ -255,35 +255,72 @@ __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restric
   }
 }
 
+// Children of one 256-parent chunk, flattened: the parents' moves are
+// compacted into LDS slots at block-scan offsets, then every lane makes one
+// child per round and stores it at chunk_base + slot -- consecutive lanes write
+// consecutive nodes (coalesced), and a ~200k-node ply keeps all lanes busy.
+constexpr u32 kWriteCap = 256 * 24;
+
+struct WriteShared {
+  Board par[256];
+  u32 pmeta[256];
+  u32 slot[kWriteCap];
+  u64 wsum[4];
+  uint16_t ptag[256];
+};
+
 template <class R, int STM>
-__global__ __launch_bounds__(256) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
-                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
-                                                     const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
-                                                     Board* __restrict__ out, uint16_t* __restrict__ out_meta,
-                                                     uint16_t* __restrict__ out_tags, u64 cap) {
-  __shared__ u64 wsum[4];
+__global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+                                                        const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
+                                                        const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
+                                                        Board* __restrict__ out, uint16_t* __restrict__ out_meta,
+                                                        uint16_t* __restrict__ out_tags, u64 cap) {
+  __shared__ WriteShared sh;
+  const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
   const u64 nch = (hi - lo + kChunk - 1) / kChunk;
   for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
-    const u64 i = lo + c * kChunk + threadIdx.x;
+    const u64 i = lo + c * kChunk + tid;
     const bool valid = i < hi;
     const u32 cnt = valid ? counts[i - lo] : 0;
-    u64 tot;
-    u64 o = block_excl_scan64<4>(cnt, wsum, &tot) + chunk_base[c];
-    if (!valid) continue;
-    const Board p = load_board(nodes, i);
-    const u32 pm = load_meta<R>(meta, i);
-    const uint16_t tag = tags[i];
-    R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
-      if (o < cap) {
-        Board ch = p;
-        const u32 cm = R::template make<STM>(ch, pm, f, t, promo);
+    u64 total64;
+    const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
+    const u32 total = (u32)total64;
+    const u64 base_out = chunk_base[c];
+    Board p{0, 0, 0, 0};
+    u32 pm = 0;
+    if (valid) {
+      p = load_board(nodes, i);
+      pm = load_meta<R>(meta, i);
+      sh.par[tid] = p;
+      if constexpr (R::kMeta) sh.pmeta[tid] = pm;
+      sh.ptag[tid] = tags[i];
+    }
+    for (u32 base = 0; base < total; base += kWriteCap) {
+      if (base) __syncthreads();  // previous window fully consumed
+      u32 j = excl;
+      if (valid && j < base + kWriteCap && j + cnt > base) {
+        R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
+          if (j >= base && j - base < kWriteCap) sh.slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (tid << 15);
+          ++j;
+        });
+      }
+      __syncthreads();
+      const u32 nslots = min(kWriteCap, total - base);
+      for (u32 r = tid; r < nslots; r += 256) {
+        const u64 o = base_out + base + r;
+        if (o >= cap) continue;
+        const u32 e = sh.slot[r];
+        const u32 pl = e >> 15;
+        Board ch = sh.par[pl];
+        const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
+                                             (int)((e >> 12) & 7));
         store_board(out, o, ch);
         if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
-        out_tags[o] = tag;
+        out_tags[o] = sh.ptag[pl];
       }
-      ++o;
-    });
+    }
+    __syncthreads();  // par/slot reused by the next chunk
   }
 }
 
@@ -438,11 +475,14 @@ __global__ __launch_bounds__(256, 4) void k_count2b(const Board* __restrict__ no
   __shared__ C2bShared sh;
   tag_hist_init(sh.hist);
   const u32 tid = threadIdx.x;
+  // Equal contiguous share of the level per resident block (the grid is one
+  // resident wave of blocks, so every CU carries the same number of parents).
   const u64 lo = rng->lo, hi = rng->hi;
-  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
-  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
-    const u64 i = lo + c * kChunk + tid;
-    const bool valid = i < hi;
+  const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;
+  const u64 blo = min(hi, lo + (u64)blockIdx.x * per), bhi = min(hi, blo + per);
+  for (u64 s = blo; s < bhi; s += kChunk) {
+    const u64 i = s + tid;
+    const bool valid = i < bhi;
     Board p{0, 0, 0, 0};
     u32 pm = 0, tag = 0;
     if (valid) {
@@ -591,7 +631,7 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
                         const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res) {
   if (plies == 1) DC_LAUNCH_RULES_STM(k_count1, grid_for(n_bound, 256), 256, st, nodes, meta, tags, rng, divide);
-  else if (res == nullptr) DC_LAUNCH_RULES_STM(k_count2b, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, divide);
+  else if (res == nullptr) DC_LAUNCH_RULES_STM(k_count2b, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
   else DC_LAUNCH_RULES_STM(k_count2, grid_for(n_bound, 64 * kC2Waves), 256, st, nodes, meta, tags, rng, divide, res);
   return hipGetLastError();
 }

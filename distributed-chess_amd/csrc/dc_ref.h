@@ -59,36 +59,55 @@ struct PawnDir {
   static constexpr int CW = STM ? -9 : 7;     // capture toward column y-1
   static constexpr int CE = STM ? -7 : 9;     // capture toward column y+1
   static constexpr u64 ROW_AFTER1 = STM ? kRow(5) : kRow(2);  // single pushes from the start row land here
+  static constexpr u64 ROW_DBL = STM ? kRow(4) : kRow(3);     // ... and double pushes land here
 };
+
+// Moves of the king(s) onto `allowed`.  One king (the norm): the 3x3 pattern
+// shifted to its square, with the wrap file masked -- one variable 64-bit
+// shift instead of eight.  Several kings (possible through the cells adapter)
+// fall back to per-direction popcounts.
+__device__ __forceinline__ u32 king_moves(u64 k, u64 allowed) {
+  if ((k & (k - 1)) == 0) {
+    if (!k) return 0;
+    const int s = lsb(k);
+    constexpr u64 kAtB2 = 0x0000000000070507ull;  // a1 b1 c1 a2 c2 a3 b3 c3 around b2 (9)
+    const u64 att = s >= 9 ? (kAtB2 << (s - 9)) : (kAtB2 >> (9 - s));
+    const int f = s & 7;
+    const u64 wrap = f == 0 ? kNotH : (f == 7 ? kNotA : kAll);
+    return pc(and3(att, wrap, allowed));
+  }
+  return pc(sh<8>(k) & allowed) + pc(sh<-8>(k) & allowed) + pc(and3(sh<1>(k), kNotA, allowed)) +
+         pc(and3(sh<-1>(k), kNotH, allowed)) + pc(and3(sh<9>(k), kNotA, allowed)) +
+         pc(and3(sh<7>(k), kNotH, allowed)) + pc(and3(sh<-7>(k), kNotA, allowed)) +
+         pc(and3(sh<-9>(k), kNotH, allowed));
+}
 
 // Bulk count of REF moves for the side to move: the number of (from,to) pairs
 // validate_move accepts.  Every term is a popcount over one direction class, so
-// multiplicity is exact (two knights reaching one square count twice).
+// multiplicity is exact (two knights reaching one square count twice).  Wrap
+// guards are applied on the target side so each leaper term is one shift, one
+// bitop3 (shifted & guard & ~own) and one popcount.
 template <int STM>
 __device__ __forceinline__ u32 ref_count(const Board& b) {
   const Sides s = sides<STM>(b);
   typedef PawnDir<STM> PD;
   const u64 push1 = sh<PD::F>(s.P) & s.empty;
-  const u64 push2 = sh<PD::F>(push1 & PD::ROW_AFTER1) & s.empty;
+  const u64 push2 = and3(sh<PD::F>(push1), PD::ROW_DBL, s.empty);
   u32 c = pc(push1) + pc(push2);
-  c += pc(sh<PD::CW>(s.P & kNotA) & s.enemy);
-  c += pc(sh<PD::CE>(s.P & kNotH) & s.enemy);
+  c += pc(and3(sh<PD::CW>(s.P), kNotH, s.enemy));  // toward column y-1: wraps land on file h
+  c += pc(and3(sh<PD::CE>(s.P), kNotA, s.enemy));  // toward column y+1: wraps land on file a
   const u64 no = s.notown;
   const u64 n = s.N;
-  c += pc(sh<17>(n & kNotH) & no) + pc(sh<15>(n & kNotA) & no);
-  c += pc(sh<10>(n & kNotGH) & no) + pc(sh<6>(n & kNotAB) & no);
-  c += pc(sh<-6>(n & kNotGH) & no) + pc(sh<-10>(n & kNotAB) & no);
-  c += pc(sh<-15>(n & kNotH) & no) + pc(sh<-17>(n & kNotA) & no);
-  const u64 k = s.K;
-  c += pc(sh<8>(k) & no) + pc(sh<-8>(k) & no);
-  c += pc(sh<1>(k & kNotH) & no) + pc(sh<-1>(k & kNotA) & no);
-  c += pc(sh<9>(k & kNotH) & no) + pc(sh<7>(k & kNotA) & no);
-  c += pc(sh<-7>(k & kNotH) & no) + pc(sh<-9>(k & kNotA) & no);
+  c += pc(and3(sh<17>(n), kNotA, no)) + pc(and3(sh<15>(n), kNotH, no));
+  c += pc(and3(sh<10>(n), kNotAB, no)) + pc(and3(sh<6>(n), kNotGH, no));
+  c += pc(and3(sh<-6>(n), kNotAB, no)) + pc(and3(sh<-10>(n), kNotGH, no));
+  c += pc(and3(sh<-15>(n), kNotA, no)) + pc(and3(sh<-17>(n), kNotH, no));
+  c += king_moves(s.K, no);
   const u64 e = s.empty;
   c += pc(ray_attacks<8, kAll>(s.O, e) & no) + pc(ray_attacks<-8, kAll>(s.O, e) & no);
-  c += pc(ray_attacks<1, kNotA>(s.O, e) & no) + pc(ray_attacks<-1, kNotH>(s.O, e) & no);
-  c += pc(ray_attacks<9, kNotA>(s.D, e) & no) + pc(ray_attacks<-9, kNotH>(s.D, e) & no);
-  c += pc(ray_attacks<7, kNotH>(s.D, e) & no) + pc(ray_attacks<-7, kNotA>(s.D, e) & no);
+  c += pc(ray_moves<1, kNotA>(s.O, e, no)) + pc(ray_moves<-1, kNotH>(s.O, e, no));
+  c += pc(ray_moves<9, kNotA>(s.D, e, no)) + pc(ray_moves<-9, kNotH>(s.D, e, no));
+  c += pc(ray_moves<7, kNotH>(s.D, e, no)) + pc(ray_moves<-7, kNotA>(s.D, e, no));
   return c;
 }
 
