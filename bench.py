@@ -29,6 +29,7 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 import numpy as np  # noqa: E402
 
 import dchess  # noqa: E402
+from dchess.dist import sharded_perft  # noqa: E402
 
 METRIC = "perft leaf nodes/sec + validated moves/sec (node), at 1/2/4/8 MI355X"
 # REF perft(startpos, d): three-way agreed (refcpu <= d4, fastcpu, GPU), tests/golden/oracle_golden.json
@@ -97,9 +98,10 @@ class Dist:
 
 
 def perft_step(eng, d, args, pos):
-    tot, div, rm = eng.perft_shard(pos, args.depth, args.split, d.rank, d.world)
-    div = d.allreduce_u64(div)
-    return int(div.sum(dtype=np.uint64)), div, rm
+    """One perft: this rank's contiguous shard of the ply-`split` frontier on its
+    GPU, then the per-root-move all-reduce (RCCL) -- dchess/dist.py."""
+    return sharded_perft(lambda p, depth, split, r, w: eng.perft_shard(p, depth, split, r, w), pos, args.depth,
+                         args.split, d.rank, d.world, reduce=d.allreduce_u64)
 
 
 def cpu_baselines(args, threads):

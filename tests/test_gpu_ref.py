@@ -286,3 +286,19 @@ def test_perft_shards_sum(engine, n_shards, split):
         acc += sd
         t += st
     assert t == tot and (acc == div).all()
+
+
+def test_multi_perft_single_device_rccl():
+    """dc_multi_perft over one device: RCCL communicator + all-reduce path."""
+    s = dchess.startpos()
+    tot, div, rm = dchess.multi_perft([0], s, 5)
+    g = OG["perft_ref"]["startpos"]["5"]
+    assert tot == g["total"]
+    assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+
+
+def test_sharded_perft_combine_single_rank(engine):
+    import dchess.dist as D
+    s = dchess.startpos()
+    tot, div, rm = D.sharded_perft(lambda p, d, sp, r, w: engine.perft_shard(p, d, sp, r, w), s, 6, 3, 0, 1)
+    assert tot == OG["perft_ref"]["startpos"]["6"]["total"]
