@@ -63,12 +63,42 @@ def random_positions(n, seed=12345, plies=(4, 60)):
     return out
 
 
+def replica_game(seed=0xD15C0, plies=80, inject=(10, 31, 52)):
+    """one scripted REF-legal game (generator, seed 0xD15C0, no
+    noise) with three illegal moves injected before plies `inject` -- one per
+    reject reason (NO_PIECE, WRONG_TURN, ILLEGAL) -- applied through refcpu
+    (chess.rs apply_move / update_history).  Every replica must reproduce the
+    verdict sequence, history string and final board."""
+    mv = O.fast_gen_games(seed, 0, 1, plies, noise_per_256=0)[:, 0]
+    cells, turn, hist = O.startpos_cells(), 0, ""
+    seq, verdicts = [], []
+    for ply, m in enumerate(mv):
+        m = int(m)
+        if m == O.SENTINEL:
+            break
+        if ply in inject:
+            want = {inject[0]: 1, inject[1]: 2, inject[2]: 3}[ply]
+            allv = O.ref_verdicts_all(cells, turn)
+            bad = int(np.flatnonzero(allv == want)[0])  # index = 64*from + to
+            seq.append([bad // 64 // 8, bad // 64 % 8, bad % 64 // 8, bad % 64 % 8])
+            v, cells, turn, hist = O.ref_apply(cells, turn, hist, *seq[-1])
+            assert v == want
+            verdicts.append(v)
+        f, t = m & 63, (m >> 6) & 63
+        seq.append([f // 8, f % 8, t // 8, t % 8])
+        v, cells, turn, hist = O.ref_apply(cells, turn, hist, *seq[-1])
+        assert v == 0
+        verdicts.append(v)
+    return {"seed": seed, "moves": seq, "verdicts": verdicts, "history": hist, "turn": turn,
+            "final_cells": [int(c) for c in cells], "final_digest": O.digest(cells, turn)}
+
+
 def main():
     golden = {}
     # ---------------------------------------------------------------- REF perft
     start = O.Pos()
     ref = {"startpos": {}}
-    for d in range(1, 7):
+    for d in range(1, 8):  # d7 (3.28e9 leaves) takes ~10 s on 8 cores
         tot, div, rm = O.fast_perft(start, d, O.REF)
         if d <= 4:
             rtot, rdiv = O.ref_perft(O.startpos_cells(), 0, d, threads=8)
@@ -87,6 +117,19 @@ def main():
             entry["perft"][str(d)] = tot
         rnd.append(entry)
     ref["random_positions"] = rnd
+    # REF-rules counts for the standard-suite FENs (castling / ep
+    # fields ignored: the reference has neither)
+    suite = {}
+    for name, (fen, _) in FIDE_SUITE.items():
+        p = O.Pos.from_fen(fen)
+        cnt = {}
+        for d in range(1, 6):
+            tot, _, _ = O.fast_perft(p, d, O.REF)
+            if d <= 2:
+                assert O.ref_perft(p.cells, p.stm, d, threads=8)[0] == tot
+            cnt[str(d)] = tot
+        suite[name] = {"fen": fen, "perft": cnt}
+    ref["suite"] = suite
     golden["perft_ref"] = ref
 
     # --------------------------------------------------------------- FIDE perft
@@ -121,6 +164,7 @@ def main():
         "stats": {"validated": int(st2[0]), "accepted": int(st2[1]), "rejected": int(st2[2]),
                   "digest_sum": int(st2[3]), "digest_xor": int(st2[4])},
     }
+    golden["replica_game"] = replica_game()
     golden["startpos_quad"] = [int(x) for x in O.quad(O.startpos_cells())]
     golden["startpos_digest"] = O.digest(O.startpos_cells(), 0)
 

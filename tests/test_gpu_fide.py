@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 OG = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))
 FIDE = dchess.RULES_FIDE
-DEPTHS = {"startpos": 5, "kiwipete": 4, "pos3": 5, "pos4": 4, "pos5": 4, "pos6": 4}
+DEPTHS = {"startpos": 5, "kiwipete": 5, "pos3": 5, "pos4": 5, "pos5": 5, "pos6": 5}  # C3: the suite at depth 5
 
 
 def dpos(p):
@@ -99,3 +99,8 @@ def test_gen_and_replay_fide(engine):
     bm, dg, st = engine.replay(mv, rules=FIDE)
     fbm, fdg, fst = O.fast_replay(mv, rules=O.FIDE)
     assert (bm == fbm).all() and (dg == fdg).all() and st["accepted"] == int(fst[1])
+
+
+def test_perft7_startpos_fide(engine):
+    """SURVEY §8d C5 (FIDE half) on one GPU: published 3,195,901,860."""
+    assert engine.perft(dchess.startpos(), 7, rules=FIDE)[0] == OG["perft_fide"]["startpos"]["perft"]["7"]

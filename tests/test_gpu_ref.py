@@ -243,7 +243,7 @@ def test_replay_device_large_properties(engine):
 
 
 # ---------------------------------------------------------------------- perft
-@pytest.mark.parametrize("depth", [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("depth", [0, 1, 2, 3, 4, 5, 6, 7])
 def test_perft_startpos_golden(engine, depth):
     tot, div, rm = engine.perft(dchess.startpos(), depth)
     if depth == 0:
@@ -302,3 +302,39 @@ def test_sharded_perft_combine_single_rank(engine):
     s = dchess.startpos()
     tot, div, rm = D.sharded_perft(lambda p, d, sp, r, w: engine.perft_shard(p, d, sp, r, w), s, 6, 3, 0, 1)
     assert tot == OG["perft_ref"]["startpos"]["6"]["total"]
+
+
+def test_perft_suite_fens_ref_rules(engine):
+    """SURVEY §8d C3, REF half: the standard-suite FENs under the reference's
+    rules (castling/ep fields carried but ignored) at depth 5."""
+    for name, e in OG["perft_ref"]["suite"].items():
+        p = dchess.pos_from_fen(e["fen"])
+        for d in ("3", "5"):
+            assert engine.perft(p, int(d))[0] == e["perft"][d], (name, d)
+
+
+# ------------------------------------------------------------- replicas (C1)
+def test_four_replicas_scripted_game():
+    """four in-process replicas (one dc_ctx each, as each
+    HotStuff peer owns its validator) apply one scripted game with three
+    injected illegal moves through the GameState mirror (chess.rs:43-98); all
+    must agree with each other and with refcpu on every verdict, the history
+    string, the final board and its digest."""
+    g = OG["replica_game"]
+    reps = [dchess.GameState("Alice", "Bob", dchess.Engine(0)) for _ in range(4)]
+    seen = []
+    for r in reps:
+        vs = []
+        for fx, fy, tx, ty in g["moves"]:
+            try:
+                r.apply_move(dchess.Position(fx, fy), dchess.Position(tx, ty))
+                vs.append(0)
+            except dchess.AppError as e:
+                vs.append({dchess.verdict_message(k): k for k in (1, 2, 3)}[str(e)])
+        cells = np.array([-1 if c is None else c.color * 8 + "PNBRQK".index(c.kind)
+                          for row in r.board for c in row], np.int8)
+        seen.append((vs, r.history, r.turn, cells.tolist()))
+    for vs, hist, turn, cells in seen:
+        assert vs == g["verdicts"] and hist == g["history"] and turn == g["turn"]
+        assert cells == g["final_cells"]
+    assert O.digest(np.array(seen[0][3], np.int8), seen[0][2]) == g["final_digest"]

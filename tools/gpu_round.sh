@@ -1,0 +1,57 @@
+#!/bin/bash
+# One full GPU round trip (run under gpurun from the repo root):
+#   1. pytest -m gpu (parity)         -> gpurun_out/pytest_gpu.log
+#   2. bench.py default (CPU legs on) -> gpurun_out/bench.json
+#   3. rocprofv3 --kernel-trace --stats of the same bench (no CPU legs) -> gpurun_out/prof/
+#   4. shard balance of perft(7)      -> gpurun_out/balance.jsonl
+#   5. PMC passes (count2b + replay)  -> gpurun_out/pmc_*/ , gpurun_out/pmc_latest.json
+# Every GPU step has its own time limit; the first failure ends the script.
+export TMPDIR=/tmp
+STAGES=${STAGES:-"test bench prof balance pmc"}
+O=gpurun_out
+has() { [[ " $STAGES " == *" $1 "* ]]; }
+step() { echo "[$(date +%T)] $*" >> $O/steps.log; }
+mkdir -p $O
+if has test; then
+  step pytest
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+  tail -2 $O/pytest_gpu.log
+fi
+if has bench; then
+  step bench
+  timeout -k 10 400 python -u bench.py ${BENCH_ARGS} > $O/bench.json 2> $O/bench.err || { cat $O/bench.err; exit 2; }
+  cat $O/bench.json
+fi
+if has prof; then
+  step prof
+  rm -rf $O/prof
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python bench.py --no-cpu ${BENCH_ARGS} > $O/bench_prof.json 2> $O/prof.err || { tail -20 $O/prof.err; exit 3; }
+fi
+if has balance; then
+  step balance
+  timeout -k 10 200 python -u tools/shard_balance.py 7 > $O/balance.jsonl 2>&1 || { cat $O/balance.jsonl; exit 4; }
+fi
+if has pmc; then
+  rm -rf $O/pmc_*
+  P="--steps 3 --warmup 1 --no-cpu --profile-only"
+  pass() {  # $1 counters, $2 tag, $3.. bench args
+    local c=$1 t=$2; shift 2
+    step "pmc $t"
+    timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P "$@" > /dev/null 2>> $O/pmc.err
+  }
+  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" p1 --no-replay && \
+  pass "FETCH_SIZE" p2 --no-replay && pass "WRITE_SIZE" p3 --no-replay && \
+  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" p4 --no-replay || { tail $O/pmc.err; exit 5; }
+  python tools/pmc_summary.py $O --json $O/pmc_perft.json --depth 7 --source "rocprofv3 --pmc, bench.py $P --no-replay" > $O/pmc_perft.txt
+  rm -rf $O/pmc_p*
+  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" r1 --no-perft --replay-steps 2 && \
+  pass "FETCH_SIZE" r2 --no-perft --replay-steps 2 && pass "WRITE_SIZE" r3 --no-perft --replay-steps 2 || { tail $O/pmc.err; exit 6; }
+  U=$(python -c "import json;print(json.load(open('$O/bench.json'))['replay']['validated_per_step'])" 2>/dev/null || echo 0)
+  python tools/pmc_summary.py $O --json $O/pmc_replay.json --replay-units $U --source "rocprofv3 --pmc, bench.py $P --no-perft --replay-steps 2" > $O/pmc_replay.txt
+  python - <<'PY'
+import json
+a = json.load(open("gpurun_out/pmc_perft.json")); a.update(json.load(open("gpurun_out/pmc_replay.json")))
+json.dump(a, open("gpurun_out/pmc_latest.json", "w"), indent=1)
+PY
+fi
+step done
