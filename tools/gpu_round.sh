@@ -39,11 +39,11 @@ if has pmc; then
     step "pmc $t"
     timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P "$@" > /dev/null 2>> $O/pmc.err
   }
-  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" p1 --no-replay && \
-  pass "FETCH_SIZE" p2 --no-replay && pass "WRITE_SIZE" p3 --no-replay && \
-  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" p4 --no-replay || { tail $O/pmc.err; exit 5; }
+  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" k1 --no-replay && \
+  pass "FETCH_SIZE" k2 --no-replay && pass "WRITE_SIZE" k3 --no-replay && \
+  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" k4 --no-replay || { tail $O/pmc.err; exit 5; }
   python tools/pmc_summary.py $O --json $O/pmc_perft.json --depth 7 --source "rocprofv3 --pmc, bench.py $P --no-replay" > $O/pmc_perft.txt
-  rm -rf $O/pmc_p*
+  rm -rf $O/pmc_k*  # pass dirs only (pmc_perft.* must survive)
   pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" r1 --no-perft --replay-steps 2 && \
   pass "FETCH_SIZE" r2 --no-perft --replay-steps 2 && pass "WRITE_SIZE" r3 --no-perft --replay-steps 2 || { tail $O/pmc.err; exit 6; }
   U=$(python -c "import json;print(json.load(open('$O/bench.json'))['replay']['validated_per_step'])" 2>/dev/null || echo 0)
