@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <map>
 #include <mutex>
 
@@ -532,6 +534,127 @@ __global__ __launch_bounds__(256, 4) void k_count2b(const Board* __restrict__ no
   tag_hist_flush(sh.hist, divide);
 }
 
+// ---------------------------------------------------- k_count2c (REF final stage)
+// The last two plies under RULES_REF with the quiet-move shortcut of
+// ref_count_nonpawn: per parent P (side S to move, opponent O) the block first
+// computes base = O's knight/king/slider moves in P and att = O's slider rays.
+// A child reached by a quiet move f -> t with f, t outside att then has
+//     count_O(child) = base + O's pawn moves in the child      (~40 VALU ops)
+// and every other child (captures, moves touching a ray) is recounted in full.
+// Those are compacted per wave into an LDS queue and recounted 64 at a time,
+// so the full count never runs with idle lanes.  At plies 6-7 of startpos
+// about 88 % of the children take the short path.
+constexpr int kC2cQueue = 128;
+
+template <u32 CAP>
+struct C2cShared {
+  Board par[256];
+  u64 att[256];
+  u32 base[256];
+  u32 slot[CAP];
+  u32 queue[4][kC2cQueue];
+  u64 hist[256];
+  u64 wsum[4];
+  uint16_t ptag[256];
+};
+
+template <int STM, u32 CAP>
+__device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
+  const u32 pl = e >> 15;
+  Board ch = sh.par[pl];
+  ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
+  return ref_count<1 - STM>(ch);
+}
+
+template <int STM, u32 CAP>
+__global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
+                                                 const Range* __restrict__ rng, u64* __restrict__ divide) {
+  __shared__ C2cShared<CAP> sh;
+  tag_hist_init(sh.hist);
+  const u32 tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+  u32* q = sh.queue[w];
+  const u64 lo = rng->lo, hi = rng->hi;
+  const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;
+  const u64 blo = min(hi, lo + (u64)blockIdx.x * per), bhi = min(hi, blo + per);
+  for (u64 s = blo; s < bhi; s += kChunk) {
+    const u64 i = s + tid;
+    const bool valid = i < bhi;
+    Board p{0, 0, 0, 0};
+    u32 tag = 0, cnt = 0, base = 0;
+    u64 att = 0;
+    if (valid) {
+      p = load_board(nodes, i);
+      tag = tags[i];
+      cnt = ref_count<STM>(p);
+      base = ref_count_nonpawn<1 - STM>(p, att);
+    }
+    u64 total64;
+    const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
+    const u32 total = (u32)total64;
+    sh.par[tid] = p;
+    sh.att[tid] = att;
+    sh.base[tid] = base;
+    sh.ptag[tid] = (uint16_t)tag;
+    __syncthreads();
+    const u32 tag0 = sh.ptag[0];
+    u64 acc = 0;  // grandchildren under parents whose tag == tag0
+    auto add = [&](u32 pl, u32 k, bool live) {
+      if (!live) return;
+      const u32 ptag = sh.ptag[pl];
+      if (ptag == tag0) acc += k;
+      else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
+    };
+    u32 qn = 0;  // wave-uniform queue length
+    for (u32 wbase = 0; wbase < total; wbase += CAP) {
+      if (wbase) __syncthreads();  // previous window fully read
+      u32 j = excl;
+      if (valid && j < wbase + CAP && j + cnt > wbase) {
+        ref_for_each_move<STM>(p, [&](int f, int t) {
+          if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
+          ++j;
+        });
+      }
+      __syncthreads();
+      const u32 nslots = min(CAP, total - wbase);
+      for (u32 r0 = w * 64; r0 < nslots; r0 += 256) {
+        const u32 r = r0 + lane;
+        const bool live = r < nslots;
+        const u32 e = live ? sh.slot[r] : 0u;
+        const u32 pl = e >> 15;
+        const int f = (int)(e & 63), t = (int)((e >> 6) & 63);
+        const Board pb = sh.par[pl];
+        const u64 a = sh.att[pl];
+        const u64 occ = occupied(pb);
+        const bool quiet = ((((occ | a) >> t) | (a >> f)) & 1) == 0;
+        const bool cheap = live && quiet;
+        if (cheap) add(pl, sh.base[pl] + ref_pawn_count_child<1 - STM>(pb, f, t), true);
+        const u64 em = ballot(live && !quiet);
+        if (live && !quiet) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = e;
+        qn += (u32)__popcll(em);
+        if (qn >= 64) {
+          wave_lds_sync();
+          const u32 e2 = q[lane];
+          add(e2 >> 15, c2c_full<STM>(sh, e2), true);
+          wave_lds_sync();
+          if (lane + 64 < qn) q[lane] = q[lane + 64];
+          qn -= 64;
+        }
+      }
+    }
+    // drain this wave's queue (par/att of the chunk are still in LDS)
+    if (qn) {
+      wave_lds_sync();
+      const bool live = lane < qn;
+      const u32 e2 = live ? q[lane] : 0u;
+      const u32 k = live ? c2c_full<STM>(sh, e2) : 0u;
+      add(e2 >> 15, k, live);
+    }
+    tag_hist_add(sh.hist, tag0, acc, true);
+    __syncthreads();  // par/att/ptag/slot reused by the next chunk
+  }
+  tag_hist_flush(sh.hist, divide);
+}
+
 // ------------------------------------------------------------- launchers
 static constexpr u32 kMaxGrid = 1u << 20;
 
@@ -628,9 +751,43 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
   return hipGetLastError();
 }
 
+// Final-stage selection (for A/B measurement): DC_FINAL=2b forces k_count2b
+// under REF; DC_C2C_CAP=20|24|28 sets k_count2c's child slots per parent.
+static int final_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("DC_FINAL");
+    return (e && std::strcmp(e, "2b") == 0) ? 0 : 1;
+  }();
+  return v;
+}
+
+template <u32 CAP>
+static void launch_count2c_cap(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
+                               u64* divide) {
+  if (stm) {
+    auto k = k_count2c<1, CAP>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide);
+  } else {
+    auto k = k_count2c<0, CAP>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide);
+  }
+}
+
+static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
+                           u64* divide) {
+  static const int cap = [] {
+    const char* e = std::getenv("DC_C2C_CAP");
+    return e ? std::atoi(e) : 24;
+  }();
+  if (cap == 20) launch_count2c_cap<256 * 20>(st, stm, nodes, tags, rng, divide);
+  else if (cap == 28) launch_count2c_cap<256 * 28>(st, stm, nodes, tags, rng, divide);
+  else launch_count2c_cap<256 * 24>(st, stm, nodes, tags, rng, divide);
+}
+
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
                         const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res) {
   if (plies == 1) DC_LAUNCH_RULES_STM(k_count1, grid_for(n_bound, 256), 256, st, nodes, meta, tags, rng, divide);
+  else if (res == nullptr && rules == 0 && final_variant() != 0) launch_count2c(st, stm, nodes, tags, rng, divide);
   else if (res == nullptr) DC_LAUNCH_RULES_STM(k_count2b, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
   else DC_LAUNCH_RULES_STM(k_count2, grid_for(n_bound, 64 * kC2Waves), 256, st, nodes, meta, tags, rng, divide, res);
   return hipGetLastError();

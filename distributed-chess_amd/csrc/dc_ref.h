@@ -111,6 +111,55 @@ __device__ __forceinline__ u32 ref_count(const Board& b) {
   return c;
 }
 
+// ------------------------------------------------ split count (k_count2c)
+// For the side SIDE in `b`: the moves of its knights, kings and sliders (the
+// part of ref_count that a quiet move of the OTHER side leaves unchanged unless
+// it touches a slider ray), and in `att` the union of its slider rays -- every
+// square a ray reaches, up to and including the first occupied one.
+//
+// Why a quiet move m = (f -> t, t empty) by the other side keeps this part: the
+// SIDE's own set is unchanged (nothing of SIDE is captured), so leaper targets
+// (not-own squares) are unchanged; a slider ray changes only if it reached f
+// (f empties, the ray now runs on) or t (t fills, the ray now stops there),
+// i.e. only if f or t is in `att`.  Then only SIDE's pawn moves need
+// recounting in the child (ref_pawn_count_child).  Checked on random positions
+// (including unknown-kind pieces) against the oracle: DESIGN.md §3.
+template <int SIDE>
+__device__ __forceinline__ u32 ref_count_nonpawn(const Board& b, u64& att) {
+  const Sides s = sides<SIDE>(b);
+  const u64 no = s.notown, n = s.N, e = s.empty;
+  u32 c = pc(and3(sh<17>(n), kNotA, no)) + pc(and3(sh<15>(n), kNotH, no));
+  c += pc(and3(sh<10>(n), kNotAB, no)) + pc(and3(sh<6>(n), kNotGH, no));
+  c += pc(and3(sh<-6>(n), kNotAB, no)) + pc(and3(sh<-10>(n), kNotGH, no));
+  c += pc(and3(sh<-15>(n), kNotA, no)) + pc(and3(sh<-17>(n), kNotH, no));
+  c += king_moves(s.K, no);
+  const u64 a0 = ray_attacks<8, kAll>(s.O, e), a1 = ray_attacks<-8, kAll>(s.O, e);
+  const u64 a2 = ray_attacks<1, kNotA>(s.O, e), a3 = ray_attacks<-1, kNotH>(s.O, e);
+  const u64 a4 = ray_attacks<9, kNotA>(s.D, e), a5 = ray_attacks<-9, kNotH>(s.D, e);
+  const u64 a6 = ray_attacks<7, kNotH>(s.D, e), a7 = ray_attacks<-7, kNotA>(s.D, e);
+  c += pc(a0 & no) + pc(a1 & no) + pc(a2 & no) + pc(a3 & no);
+  c += pc(a4 & no) + pc(a5 & no) + pc(a6 & no) + pc(a7 & no);
+  att = bop3<0xFE>(bop3<0xFE>(a0, a1, a2), bop3<0xFE>(a3, a4, a5), a6 | a7);  // 0xFE = a | b | c
+  return c;
+}
+
+// Pawn moves of SIDE in the child reached from `b` by the other side's quiet
+// move f -> t (f occupied by the mover, t empty): the pawn terms of ref_count
+// on the child's occupancy, without making the child.
+template <int SIDE>
+__device__ __forceinline__ u32 ref_pawn_count_child(const Board& b, int f, int t) {
+  typedef PawnDir<SIDE> PD;
+  const u64 occ = occupied(b);
+  const u64 own = SIDE ? b.b0 : (occ & ~b.b0);
+  const u64 P = and_andn(own, b.b1, b.b2 | b.b3);
+  const u64 ft = (1ull << f) | (1ull << t);
+  const u64 empty_c = ~(occ ^ ft);
+  const u64 enemy_c = (occ & ~own) ^ ft;  // the mover's pieces after the move
+  const u64 push1 = sh<PD::F>(P) & empty_c;
+  const u64 push2 = and3(sh<PD::F>(push1), PD::ROW_DBL, empty_c);
+  return pc(push1) + pc(push2) + pc(and3(sh<PD::CW>(P), kNotH, enemy_c)) + pc(and3(sh<PD::CE>(P), kNotA, enemy_c));
+}
+
 // Runtime side-to-move version.
 __device__ __forceinline__ u32 ref_count_rt(const Board& b, u32 stm) {
   return stm ? ref_count<1>(b) : ref_count<0>(b);

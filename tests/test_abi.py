@@ -23,6 +23,22 @@ def test_library_exports_every_header_symbol():
         assert hasattr(L, n), n
 
 
+def test_rust_binding_matches_header():
+    """integration/rust/src/lib.rs (unverified: no cargo here) declares only
+    symbols the header declares, with the same parameter count."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(dchess.LIB_PATH), "..", "include", "dchess.h")).read()
+    rs = open(os.path.join(os.path.dirname(dchess.LIB_PATH), "..", "integration", "rust", "src", "lib.rs")).read()
+    hdr_args = {m.group(1): len([a for a in m.group(2).split(",") if a.strip() not in ("", "void")])
+                for m in re.finditer(r"(dc_\w+)\s*\(([^)]*)\)\s*;", hdr)}
+    rs_fns = {m.group(1): len([a for a in m.group(2).split(",") if a.strip()])
+              for m in re.finditer(r"pub fn (dc_\w+)\(([^)]*)\)", rs)}
+    assert len(rs_fns) >= 15
+    for name, n in rs_fns.items():
+        assert name in hdr_args, name
+        assert hdr_args[name] == n, (name, hdr_args[name], n)
+
+
 def test_version_and_messages():
     assert dchess.lib().dc_version() >= 100
     # exact reference strings, chess.rs:104-121

@@ -45,8 +45,8 @@ def hbm(c):
 if a.json:
     out = {}
     for k, c in avg.items():
-        if "k_count2b<dc::RefRules" in k:
-            out[f"count2b_d{a.depth}"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
+        if "k_count2b<dc::RefRules" in k or "k_count2c<" in k:  # the REF final stage
+            out[f"final_d{a.depth}"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
                                           "valu_lane_ops_per_leaf": c.get("SQ_INSTS_VALU", 0) * 64 / REF[a.depth],
                                           "counters_per_dispatch": c, "source": a.source}
         if "k_replay_ref" in k and a.replay_units:
