@@ -604,41 +604,71 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       if (ptag == tag0) acc += k;
       else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
     };
-    u32 qn = 0;  // wave-uniform queue length
+    u32 qn = 0;  // queue length: wave-uniform (kept scalar via readfirstlane)
+    // One candidate child: its parent's LDS record is loaded first (so two
+    // candidates' loads can be in flight together), then the short path if the
+    // move is quiet, else the child is appended to the queue.
+    struct Cand {
+      u32 e, base;
+      Board pb;
+      u64 a;
+    };
+    auto fetch = [&](u32 e) {
+      const u32 pl = e >> 15;
+      return Cand{e, sh.base[pl], sh.par[pl], sh.att[pl]};
+    };
+    auto consume = [&](const Cand& c, bool live) {
+      const u32 pl = c.e >> 15;
+      const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
+      const u64 occ = occupied(c.pb);
+      const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
+      if (live && quiet) add(pl, c.base + ref_pawn_count_child<1 - STM>(c.pb, f, t), true);
+      const bool full = live && !quiet;
+      const u64 em = ballot(full);
+      if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
+      qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
+    };
+    auto drain64 = [&]() {  // qn >= 64: recount 64 queued children in full
+      wave_lds_sync();
+      const u32 e2 = q[lane];
+      add(e2 >> 15, c2c_full<STM>(sh, e2), true);
+      wave_lds_sync();
+      if (lane + 64 < qn) q[lane] = q[lane + 64];
+      qn = __builtin_amdgcn_readfirstlane(qn - 64);
+    };
     for (u32 wbase = 0; wbase < total; wbase += CAP) {
       if (wbase) __syncthreads();  // previous window fully read
-      u32 j = excl;
-      if (valid && j < wbase + CAP && j + cnt > wbase) {
-        ref_for_each_move<STM>(p, [&](int f, int t) {
-          if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
-          ++j;
-        });
+      if (total <= CAP) {  // the norm: one window, no range checks
+        u32 j = excl;
+        if (valid) ref_for_each_move<STM>(p, [&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | (tid << 15); });
+      } else {
+        u32 j = excl;
+        if (valid && j < wbase + CAP && j + cnt > wbase) {
+          ref_for_each_move<STM>(p, [&](int f, int t) {
+            if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
+            ++j;
+          });
+        }
       }
       __syncthreads();
       const u32 nslots = min(CAP, total - wbase);
-      for (u32 r0 = w * 64; r0 < nslots; r0 += 256) {
-        const u32 r = r0 + lane;
-        const bool live = r < nslots;
-        const u32 e = live ? sh.slot[r] : 0u;
-        const u32 pl = e >> 15;
-        const int f = (int)(e & 63), t = (int)((e >> 6) & 63);
-        const Board pb = sh.par[pl];
-        const u64 a = sh.att[pl];
-        const u64 occ = occupied(pb);
-        const bool quiet = ((((occ | a) >> t) | (a >> f)) & 1) == 0;
-        const bool cheap = live && quiet;
-        if (cheap) add(pl, sh.base[pl] + ref_pawn_count_child<1 - STM>(pb, f, t), true);
-        const u64 em = ballot(live && !quiet);
-        if (live && !quiet) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = e;
-        qn += (u32)__popcll(em);
-        if (qn >= 64) {
-          wave_lds_sync();
-          const u32 e2 = q[lane];
-          add(e2 >> 15, c2c_full<STM>(sh, e2), true);
-          wave_lds_sync();
-          if (lane + 64 < qn) q[lane] = q[lane + 64];
-          qn -= 64;
-        }
+      // two slots per lane per step, loaded together, so the LDS round trips overlap
+      u32 r0 = w * 64;
+      for (; r0 + 256 < nslots; r0 += 512) {
+        const u32 ra = r0 + lane, rb = r0 + 256 + lane;
+        const bool lb = rb < nslots;
+        const Cand ca = fetch(sh.slot[ra]);
+        const Cand cb = fetch(lb ? sh.slot[rb] : 0u);
+        consume(ca, true);
+        if (qn >= 64) drain64();
+        consume(cb, lb);
+        if (qn >= 64) drain64();
+      }
+      if (r0 < nslots) {
+        const u32 ra = r0 + lane;
+        const bool la = ra < nslots;
+        consume(fetch(la ? sh.slot[ra] : 0u), la);
+        if (qn >= 64) drain64();
       }
     }
     // drain this wave's queue (par/att of the chunk are still in LDS)
