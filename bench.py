@@ -194,35 +194,63 @@ def profiled_perft(eng, d, args, pos, depth, steps):
     return {k: eng.kernel_stats(k) for k in ("expand_top", "expand_count", "scan", "expand_write", "count2")}
 
 
+def _pmc(key):
+    """The committed PMC record (profiles/pmc_latest.json) of one kernel, or None."""
+    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
+    if not os.path.exists(pmc):
+        return None
+    return json.load(open(pmc)).get(key)
+
+
+def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key):
+    """Bound: int32 VALU issue.  achieved = units/s x W, where W =
+    VALU lane-ops per unit executed by THIS kernel (rocprofv3 SQ_INSTS_VALU x 64
+    / units, committed under profiles/), so frac = the fraction of the VALU
+    issue peak the kernel runs at.  W_frozen (the first parity-passing kernel's
+    count) is reported beside it: rate x W_frozen / peak exceeds 1
+    once a kernel needs fewer ops per unit than the first one did."""
+    w = pmc_rec[w_key] if pmc_rec else w_frozen
+    roof = {"bound": "valu", "kernel": kernel, "unit": "TOPS (int32 VALU lane-ops/s)",
+            "achieved": rate * w / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+            f"W_lane_ops_per_{unit_name}": w,
+            "W_source": pmc_rec["source"] if pmc_rec else "frozen (no PMC record for this kernel)",
+            f"W_frozen_per_{unit_name}": w_frozen,
+            "frozen_W_frac": rate * w_frozen / VALU_PEAK_LANE_OPS,
+            "traffic": pmc_rec["hbm_bytes_per_launch"] if pmc_rec else None}
+    roof["frac"] = roof["achieved"] / roof["peak"]
+    return roof
+
+
+def replay_roof(kr, n_games):
+    """k_replay_ref3 (DC_REPLAY=1: k_replay_ref).  HBM: 2 B in (u16 move) + 1/8 B
+    out (accept bit) per validated move, plus 8 B of digest per game."""
+    kernel = "k_replay_ref" if os.environ.get("DC_REPLAY") == "1" else "k_replay_ref3"
+    rec = _pmc("replay")
+    if rec and rec.get("kernel", "").split("<")[0].replace("dc::", "") != kernel:
+        rec = None
+    roof = valu_roof(kernel, kr, "move", W_REPLAY, rec, "valu_lane_ops_per_move")
+    roof["hbm"] = {"algorithmic_bytes_per_move": 2.125, "achieved_GBps": kr * 2.125 / 1e9,
+                   "peak_GBps": HBM_PEAK_GBPS, "frac": kr * 2.125 / 1e9 / HBM_PEAK_GBPS}
+    return roof
+
+
 def roofline(ks, depth, world):
     """Dominant kernel = the REF final stage (k_count2c: the last two plies, ~85 % of a step).
-    Bound: int32 VALU issue.  achieved = leaves/s x W_COUNT2 (W
-    frozen per SURVEY §8d); frac = achieved / VALU peak.  Beside it, from the
-    committed PMC passes of this depth (profiles/pmc_latest.json): the executed
-    lane-ops per leaf and the VALU-issue fraction they imply at the measured
-    kernel time, and traffic = HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE).
+    traffic = HBM bytes per launch from the PMC passes (2 x FETCH_SIZE + WRITE_SIZE).
     The HBM side: algorithmic bytes = frontier positions x 40 B read per launch."""
     c2 = ks["count2"]
     avg_s = c2["total_ms"] / max(c2["launches"], 1) / 1e3
     leaves = c2["units"] / max(c2["launches"], 1)
     rate = leaves / avg_s if avg_s > 0 else 0.0
-    roof = {"bound": "valu", "kernel": FINAL_KERNEL, "unit": "TOPS (int32 VALU lane-ops/s)",
-            "achieved": rate * W_COUNT2 / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-            "W_lane_ops_per_leaf": W_COUNT2, "kernel_avg_ms": avg_s * 1e3, "kernel_leaves_per_s": rate,
-            "traffic": None}
-    roof["frac"] = roof["achieved"] / roof["peak"]
+    rec = _pmc(f"final_d{depth}") if world == 1 else None
+    if rec and FINAL_KERNEL not in rec.get("kernel", ""):
+        rec = None  # PMC of another final-stage kernel
+    roof = valu_roof(FINAL_KERNEL, rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
+    roof.update({"kernel_avg_ms": avg_s * 1e3, "kernel_leaves_per_s": rate})
     frontier = REF_STARTPOS[depth - 2] / world  # ply depth-2 positions read by one launch (exact at N=1)
     alg_bytes = frontier * POS_BYTES
     roof["hbm"] = {"algorithmic_bytes_per_launch": alg_bytes, "achieved_GBps": alg_bytes / avg_s / 1e9,
                    "peak_GBps": HBM_PEAK_GBPS, "frac": alg_bytes / avg_s / 1e9 / HBM_PEAK_GBPS}
-    pmc = os.path.join(REPO, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc) and world == 1:
-        p = json.load(open(pmc)).get(f"final_d{depth}")
-        if p:
-            roof["traffic"] = p["hbm_bytes_per_launch"]
-            w = p["valu_lane_ops_per_leaf"]
-            roof["pmc"] = {"executed_lane_ops_per_leaf": w, "executed_TOPS": rate * w / 1e12,
-                           "valu_issue_frac": rate * w / VALU_PEAK_LANE_OPS, "source": p["source"]}
     return roof
 
 
@@ -277,12 +305,7 @@ def main():
                               "moves, game ids partitioned by rank)",
                   "scaling": "weak", "ms_per_step": 1e3 * rdt / args.replay_steps,
                   "kernel_avg_ms": avg_s * 1e3, "kernel_moves_per_s": kr, "validated_per_step": st["validated"],
-                  "roofline": {"bound": "valu", "kernel": "k_replay_ref", "unit": "TOPS (int32 VALU lane-ops/s)",
-                               "W_lane_ops_per_move": W_REPLAY, "achieved": kr * W_REPLAY / 1e12,
-                               "peak": VALU_PEAK_LANE_OPS / 1e12,
-                               "frac": kr * W_REPLAY / VALU_PEAK_LANE_OPS,
-                               "hbm": {"algorithmic_bytes_per_move": 2.125,
-                                       "achieved_GBps": kr * 2.125 / 1e9, "peak_GBps": HBM_PEAK_GBPS}},
+                  "roofline": replay_roof(kr, n),
                   "bitmap_checksum": {"accepted": st["accepted"], "digest_xor": st["digest_xor"]}}
         for b in (d_moves, d_bm, d_dg):
             b.free()

@@ -4,6 +4,8 @@
 //   k_apply_{ref,fide}      K2': validate + make in place           -> verdict, info
 //   k_replay_{ref,fide}     K1: one lane per game, loop over plies  -> ply-major accept bitmap
 //   k_gen_games_{ref,fide}  K5: one lane per game, seeded games     -> ply-major moves
+#include <algorithm>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include "dc_common.h"
@@ -151,6 +153,217 @@ __global__ __launch_bounds__(256) void k_replay_ref(Board start, u32 stm0, const
     if (digests) digests[g] = d;
   }
   block_stats(validated, accepted, d, partial);
+}
+
+// ------------------------------------------- replay, LDS table + LDS mailbox
+// k_replay_ref3 gives the verdicts of ref_verdict with the geometry of every
+// (from, to) pair read from a 48 KB table staged in LDS, indexed by the move
+// word's low 12 bits (m & 0xFFF = f | t << 6):
+//   btw[e]  squares strictly between f and t when aligned (the path walks of
+//           chess.rs:272-284 / :322-332; the mid square of a double push,
+//           :240-246), 0 otherwise -- so "path clear" is (btw & occ) == 0 for
+//           every kind, and one test covers sliders and double pushes
+//   geo[e]  bit n set iff a piece of nibble n (black | kind << 1) may move
+//           f -> t onto an empty t; bit 16 + n iff onto an enemy piece.  Pawns
+//           differ between the two (push / double from row 1 or 6 vs the
+//           forward diagonal, chess.rs:235-251); knights, kings and sliders
+//           do not (chess.rs:289-360).  Empty squares and unknown kinds have
+//           no bits (chess.rs:101-108, :211).
+// The mover's colour (WRONG_TURN, chess.rs:112-116) and an own piece on t
+// (chess.rs:286, :334, :299, :359, :236) are two 16-entry bit LUTs on
+// nibble(t) ^ stm.  Each game's board is a nibble mailbox in LDS (8 dwords per
+// lane, dword-major [j][thread] so every lane owns its bank: conflict-free)
+// beside an occupancy bitboard in registers: the nibbles of f and t are two
+// ds_read_b32 + v_bfe, and make-move (chess.rs:72-77) is two ds_xor_b32 (XOR
+// deltas commute, so f and t in one dword need no special case) plus the
+// occupancy update.  The quad-bitboard is rebuilt once per game for the digest.
+// Per ply: ~40 VALU ops against ~175 for ref_verdict on registers.
+constexpr u32 kR3Threads = 1024;
+constexpr u32 kR3TabBytes = 4096 * 8 + 4096 * 4;  // btw (32 KB) + geo (16 KB)
+constexpr u32 kR3MbBytes = 8 * kR3Threads * 4;      // 32 KB: two blocks fill a CU's 160 KB
+constexpr u32 kEnemyLut = 0xAAA8u;  // x = nibble(t) ^ stm: occupied (x >= 2) by the other side (x odd)
+constexpr u32 kOwnLut = 0x5554u;    // ... by the side to move (x even)
+
+__device__ __forceinline__ u32 replay_geo(u32 e) {
+  const int f = (int)(e & 63), t = (int)(e >> 6);
+  const int dx = (t >> 3) - (f >> 3), dy = (t & 7) - (f & 7);
+  const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
+  const bool knight = (ax == 1 && ay == 2) || (ax == 2 && ay == 1);
+  const bool king = ax <= 1 && ay <= 1 && (ax | ay) != 0;
+  const bool diag = ax == ay && ax != 0;
+  const bool orth = (dx == 0) != (dy == 0);
+  u32 both = 0;  // kinds whose quiet and capture geometry agree, both colours
+  auto cls = [](u32 kind) { return 3u << (kind << 1); };
+  if (knight) both |= cls(KC_N);
+  if (king) both |= cls(KC_K);
+  if (diag) both |= cls(KC_B) | cls(KC_Q);
+  if (orth) both |= cls(KC_R) | cls(KC_Q);
+  const u32 wp = 1u << (KC_P << 1), bp = wp << 1;
+  u32 quiet = both, cap = both;
+  if (dy == 0 && (dx == 1 || (dx == 2 && (f >> 3) == 1))) quiet |= wp;
+  if (dy == 0 && (dx == -1 || (dx == -2 && (f >> 3) == 6))) quiet |= bp;
+  if (ay == 1 && dx == 1) cap |= wp;
+  if (ay == 1 && dx == -1) cap |= bp;
+  return quiet | (cap << 16);
+}
+
+// v_writelane_b32: lane `sel` (wave-uniform) of `old` <- the uniform `val`.
+__device__ __forceinline__ u32 writelane(u32 old, u32 val, u32 sel) {
+  // gfx9's constant bus takes one SGPR per VALU op: the lane select goes through M0
+  asm volatile("s_mov_b32 m0, %2\n\tv_writelane_b32 %0, %1, m0" : "+v"(old) : "s"(val), "s"(sel) : "m0");
+  return old;
+}
+
+// Nibble-spaced bits (0, 4, ..., 28) of x gathered into bits 0..7.
+__device__ __forceinline__ u32 gather_nibble_bits(u32 x) {
+  x &= 0x11111111u;
+  x = (x | (x >> 3)) & 0x03030303u;
+  x = (x | (x >> 6)) & 0x000F000Fu;
+  return (x | (x >> 12)) & 0xFFu;
+}
+
+// The start position's mailbox, packed on the host (kernel argument: SGPRs).
+struct Mailbox {
+  u32 d[8];
+};
+
+__global__ __launch_bounds__(kR3Threads) void k_replay_ref3(Mailbox mb0, u64 occ0, u32 stm0, const uint16_t* __restrict__ moves,
+                                                           u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
+                                                           u64* __restrict__ digests, u64* __restrict__ partial) {
+  // static (not extern) LDS: its base is the constant 0, folded into the ds offsets
+  __shared__ __attribute__((aligned(16))) unsigned char r3_smem[kR3TabBytes + kR3MbBytes];
+  u64* btw = reinterpret_cast<u64*>(r3_smem);
+  u32* mb = reinterpret_cast<u32*>(r3_smem + kR3TabBytes);  // mb[j * kR3Threads + tid]
+  const u32 tid = threadIdx.x;
+  for (u32 e = tid; e < 4096; e += kR3Threads) {
+    btw[e] = between((int)(e & 63), (int)(e >> 6));
+    reinterpret_cast<u32*>(r3_smem + 4096 * 8)[e] = replay_geo(e);
+  }
+  __syncthreads();
+  const u32 lane = lane_id();
+  const u32 words = (n_games + 63) >> 6;
+  const u32 tid4 = tid * 4;       // byte offset of this lane's mailbox column
+  const u32 last = n_plies - 1;   // n_plies >= 1 (the launcher routes n_plies == 0 elsewhere)
+  u32* my = mb + tid;
+  u32 validated = 0, accepted = 0;
+  u64 dsum = 0, dxor = 0;
+  // Block-contiguous chunks: in round r, block b's 16 waves take the 16
+  // consecutive 64-game chunks (r * grid + b) * 16 + w, so a block reads 2 KB
+  // runs of every ply row and concurrently running blocks sweep one region of
+  // each row.  Per-wave dynamic chunks scattered the 128-B reads over DRAM
+  // pages: 1.65x slower.
+  for (u32 round = 0;; ++round) {
+    const u32 c = (round * gridDim.x + blockIdx.x) * (kR3Threads / 64) + (tid >> 6);
+    if (c >= words) break;
+    const u32 g = (c << 6) | lane;
+    const bool active = g < n_games;
+    // byte offset of this lane's game in a ply row; inactive lanes (last chunk
+    // only) read game n-1 and are masked, so every load is unconditional
+    const u32 goff = (active ? g : n_games - 1) * 2;
+    // buffer_load with the ply row's base in an SGPR descriptor and the lane's
+    // 32-bit offset in a VGPR: no 64-bit address arithmetic per ply
+    auto load_move = [&](u32 p) -> u32 {
+      const uint16_t* row = moves + (size_t)min(p, last) * n_games;  // uniform
+      const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)row, 0, n_games * 2, 0x00020000);
+      return __builtin_amdgcn_raw_buffer_load_b16(r, goff, 0, 0);
+    };
+#pragma unroll
+    for (u32 j = 0; j < 8; ++j) my[j * kR3Threads] = mb0.d[j];
+    u64 occ = occ0;
+    u32 stm = stm0;
+    u32 buf[kReplayPrefetch];
+#pragma unroll
+    for (int k = 0; k < kReplayPrefetch; ++k) buf[k] = load_move((u32)k);
+    u32 bw_lo = 0, bw_hi = 0;  // lane j holds the ballot word of ply 64q + j
+    for (u32 ply = 0; ply < n_plies; ply += kReplayPrefetch) {
+#pragma unroll
+      for (int k = 0; k < kReplayPrefetch; ++k) {
+        const u32 pl = ply + k;
+        const u32 m = (active && pl < n_plies) ? buf[k] : 0xFFFFu;
+        buf[k] = load_move(pl + kReplayPrefetch);
+        const u32 m2 = m << 2, m3 = m << 3;
+        const u64 bt = *reinterpret_cast<const u64*>(r3_smem + (m3 & 0x7FF8u));             // btw[m & 0xFFF]
+        const u32 gw = *reinterpret_cast<const u32*>(r3_smem + 4096 * 8 + (m2 & 0x3FFCu));  // geo[m & 0xFFF]
+        // mailbox dwords of f and t: ((square >> 3) << 12) | tid4, one bitop3 each
+        const u32 af = __builtin_amdgcn_bitop3_b32(m << 9, tid4, 0x7000u, 0xE4);  // (a & c) | (b & ~c)
+        const u32 at = __builtin_amdgcn_bitop3_b32(m3, tid4, 0x7000u, 0xE4);
+        const u32 wf = *reinterpret_cast<const u32*>(r3_smem + kR3TabBytes + af);
+        const u32 wt = *reinterpret_cast<const u32*>(r3_smem + kR3TabBytes + at);
+        const u32 st = (m >> 4) & 28;
+        const u32 nib = __builtin_amdgcn_ubfe(wf, m2, 4);  // v_bfe reads offset bits 4:0 = (f & 7) * 4
+        const u32 nibt = __builtin_amdgcn_ubfe(wt, st, 4);
+        const u32 x = nibt ^ stm;
+        const u32 shift = nib | (__builtin_amdgcn_ubfe(kEnemyLut, x, 1) << 4);
+        // bit 0 of bad: wrong geometry for the target's state, own piece on t,
+        // mover not of the side to move (or no piece), or an OOR/sentinel word
+        const u32 geo_ok = __builtin_amdgcn_ubfe(gw, shift, 1), own = __builtin_amdgcn_ubfe(kOwnLut, x, 1);
+        const u32 okb = __builtin_amdgcn_bitop3_b32(geo_ok, own, __builtin_amdgcn_bitop3_b32(nib, stm, m >> 15, 0xBE),
+                                                    0x10);  // a & ~b & ~c, c = (nib ^ stm) | m >> 15 (0xBE): only bit 0 can be set
+        const bool ok = okb != 0 && (bt & occ) == 0;
+        const u64 w = ballot(ok);  // before the branch: the mask is the compare's own result
+        if (ok) {
+          atomicXor(reinterpret_cast<u32*>(r3_smem + kR3TabBytes + af), nib << m2);  // ds_xor_b32: f empties
+          atomicXor(reinterpret_cast<u32*>(r3_smem + kR3TabBytes + at), (nib ^ nibt) << st);  // t <- mover
+          occ = bop3<0xBA>(occ, 1ull << (m & 63), 1ull << ((m >> 6) & 63));  // (occ & ~f) | t
+          stm ^= 1;
+        }
+        // per-lane counters: ballot popcounts (s_bcnt1 + 64-bit s_add) put ~8 SALU
+        // on every ply's critical issue path and cost 20 % (A/B)
+        validated += (m != 0xFFFFu);
+        accepted += ok;
+        const u32 slot = pl & 63;
+        bw_lo = writelane(bw_lo, (u32)w, slot);
+        bw_hi = writelane(bw_hi, (u32)(w >> 32), slot);
+      }
+      // every 64 plies (and at the end) lane j stores the word of ply base + j
+      const u32 done = min(ply + kReplayPrefetch, n_plies);
+      if (bitmap && ((done & 63) == 0 || done == n_plies)) {
+        const u32 base = (done - 1) & ~63u;
+        if (lane < done - base) bitmap[(size_t)(base + lane) * words + c] = ((u64)bw_hi << 32) | bw_lo;
+      }
+    }
+    if (active) {
+      Board b{0, 0, 0, 0};
+#pragma unroll
+      for (u32 j = 0; j < 8; ++j) {
+        const u32 d = my[j * kR3Threads];
+        b.b0 |= (u64)gather_nibble_bits(d) << (8 * j);
+        b.b1 |= (u64)gather_nibble_bits(d >> 1) << (8 * j);
+        b.b2 |= (u64)gather_nibble_bits(d >> 2) << (8 * j);
+        b.b3 |= (u64)gather_nibble_bits(d >> 3) << (8 * j);
+      }
+      const u64 dg = board_digest(b, stm);
+      if (digests) digests[g] = dg;
+      dsum += dg;
+      dxor ^= dg;
+    }
+  }
+  // block partial {validated, accepted, rejected, digest sum, digest xor}
+  const u64 sv = wave_sum64(validated), sa = wave_sum64(accepted), sd = wave_sum64(dsum);
+  u64 xx = dxor;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) xx ^= __shfl_xor(xx, o, 64);
+  __syncthreads();  // the table's LDS is reused for the per-wave sums
+  u64* ws = btw;
+  const u32 w = tid >> 6;
+  if (lane == 0) {
+    ws[w * 4 + 0] = sv;
+    ws[w * 4 + 1] = sa;
+    ws[w * 4 + 2] = sd;
+    ws[w * 4 + 3] = xx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    u64 r[5] = {0, 0, 0, 0, 0};
+    for (u32 k = 0; k < kR3Threads / 64; ++k) {
+      r[0] += ws[k * 4 + 0];
+      r[1] += ws[k * 4 + 1];
+      r[3] += ws[k * 4 + 2];
+      r[4] ^= ws[k * 4 + 3];
+    }
+    r[2] = r[0] - r[1];
+    for (int k = 0; k < 5; ++k) partial[(size_t)blockIdx.x * 5 + k] = r[k];
+  }
 }
 
 // --------------------------------------------------------------- generator
@@ -325,11 +538,55 @@ hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, 
   return hipGetLastError();
 }
 
+// Partials of either replay kernel: one record per block (k_replay_ref3's
+// persistent grid is far smaller than k_replay_ref's).
 u32 replay_partials(u32 n_games) { return blocks_for(n_games, 256); }
+
+// DC_REPLAY=1 selects the arithmetic k_replay_ref (ref_verdict per ply, as the
+// validate kernels) instead of the LDS-table k_replay_ref3, for A/B and parity.
+static bool replay_arith() {
+  static const bool v = [] {
+    const char* e = std::getenv("DC_REPLAY");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static u32 replay3_grid(u32 n_games) {
+  static const u32 resident = [] {
+    int per_cu = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_replay_ref3, (int)kR3Threads, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
+    return (u32)(per_cu * cus);
+  }();
+  const u32 chunks = blocks_for(n_games, 64);
+  return std::max<u32>(1, std::min<u32>(resident, blocks_for(chunks, kR3Threads / 64)));
+}
+
+static Mailbox host_mailbox(const Board& b) {
+  Mailbox r{};
+  for (int s = 0; s < 64; ++s) {
+    const u32 n = (u32)(((b.b0 >> s) & 1) | (((b.b1 >> s) & 1) << 1) | (((b.b2 >> s) & 1) << 2) |
+                        (((b.b3 >> s) & 1) << 3));
+    r.d[s >> 3] |= n << (4 * (s & 7));
+  }
+  return r;
+}
 
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                              u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial) {
   if (n_games == 0) return hipSuccess;
+  // n_plies == 0 (no moves buffer to clamp loads into) takes k_replay_ref
+  if (n_plies > 0 && !replay_arith()) {
+    const u32 nb = replay3_grid(n_games);
+    hipLaunchKernelGGL(k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start),
+                       start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap, digests, partial);
+    hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats);
+    return hipGetLastError();
+  }
   const u32 nb = blocks_for(n_games, 256);
   hipLaunchKernelGGL(k_replay_ref, dim3(nb), dim3(256), 0, st, start, stm0, moves, n_games, n_plies, bitmap, digests,
                      partial);
