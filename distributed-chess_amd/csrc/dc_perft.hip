@@ -566,7 +566,14 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
   return ref_count<1 - STM>(ch);
 }
 
-template <int STM, u32 CAP>
+// BULK: children reached by "simple" moves -- quiet, f and t off the
+// opponent's slider rays and off its pawn-sensitive squares G
+// (ref_pawn_sensitive) -- all have count_O = base + pawn_O(parent), so they are
+// counted per parent as n_simple x (base + pawn_O) and never enumerated; only
+// the other ("special") children go through the LDS slots.
+// PHASE (timing experiments only; wrong counts unless 0): 1 skips the children,
+// 2 also skips the enumeration, leaving the per-parent counts.
+template <int STM, u32 CAP, int PHASE = 0, bool BULK = true>
 __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, u64* __restrict__ divide) {
   __shared__ C2cShared<CAP> sh;
@@ -581,12 +588,22 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
     const bool valid = i < bhi;
     Board p{0, 0, 0, 0};
     u32 tag = 0, cnt = 0, base = 0;
-    u64 att = 0;
+    u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
     if (valid) {
       p = load_board(nodes, i);
       tag = tags[i];
       cnt = ref_count<STM>(p);
       base = ref_count_nonpawn<1 - STM>(p, att);
+      if constexpr (BULK) {
+        u32 pawn_o = 0;
+        const u64 keep = ~(att | ref_pawn_sensitive<1 - STM>(p, pawn_o));
+        const Sides sd = sides<STM>(p);
+        Fs = sd.own & keep;
+        Ts = sd.empty & keep;
+        const u32 n_simple = ref_count_simple<STM>(p, Fs, Ts);
+        cnt -= n_simple;  // enumerated (special) children only
+        simple_leaves = (u64)n_simple * (base + pawn_o);
+      }
     }
     u64 total64;
     const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
@@ -636,15 +653,22 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       if (lane + 64 < qn) q[lane] = q[lane + 64];
       qn = __builtin_amdgcn_readfirstlane(qn - 64);
     };
-    for (u32 wbase = 0; wbase < total; wbase += CAP) {
+    if constexpr (BULK) add(tid, (u32)simple_leaves, valid);
+    if constexpr (PHASE != 0) acc += cnt + base + (u32)att;
+    for (u32 wbase = 0; wbase < (PHASE == 2 ? 0u : total); wbase += CAP) {
       if (wbase) __syncthreads();  // previous window fully read
+      // each (f, t) of this parent's enumerated (BULK: special) moves -> visit(f, t)
+      auto each_move = [&](auto&& visit) {
+        if constexpr (BULK) ref_for_each_special<STM>(p, Fs, Ts, visit);
+        else ref_for_each_move<STM>(p, visit);
+      };
       if (total <= CAP) {  // the norm: one window, no range checks
         u32 j = excl;
-        if (valid) ref_for_each_move<STM>(p, [&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | (tid << 15); });
+        if (valid) each_move([&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | (tid << 15); });
       } else {
         u32 j = excl;
         if (valid && j < wbase + CAP && j + cnt > wbase) {
-          ref_for_each_move<STM>(p, [&](int f, int t) {
+          each_move([&](int f, int t) {
             if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
             ++j;
           });
@@ -653,7 +677,7 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       __syncthreads();
       const u32 nslots = min(CAP, total - wbase);
       // two slots per lane per step, loaded together, so the LDS round trips overlap
-      u32 r0 = w * 64;
+      u32 r0 = PHASE ? nslots : w * 64;
       for (; r0 + 256 < nslots; r0 += 512) {
         const u32 ra = r0 + lane, rb = r0 + 256 + lane;
         const bool lb = rb < nslots;
@@ -791,27 +815,30 @@ static int final_variant() {
   return v;
 }
 
-template <u32 CAP>
+template <u32 CAP, int PHASE, bool BULK>
 static void launch_count2c_cap(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
                                u64* divide) {
   if (stm) {
-    auto k = k_count2c<1, CAP>;
+    auto k = k_count2c<1, CAP, PHASE, BULK>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide);
   } else {
-    auto k = k_count2c<0, CAP>;
+    auto k = k_count2c<0, CAP, PHASE, BULK>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide);
   }
 }
 
 static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
                            u64* divide) {
-  static const int cap = [] {
-    const char* e = std::getenv("DC_C2C_CAP");
-    return e ? std::atoi(e) : 24;
+  // DC_C2C_PHASE (A/B and timing only): 3 = no bulk split; 1, 2 = partial phases
+  static const int phase = [] {
+    const char* e = std::getenv("DC_C2C_PHASE");
+    return e ? std::atoi(e) : 0;
   }();
-  if (cap == 20) launch_count2c_cap<256 * 20>(st, stm, nodes, tags, rng, divide);
-  else if (cap == 28) launch_count2c_cap<256 * 28>(st, stm, nodes, tags, rng, divide);
-  else launch_count2c_cap<256 * 24>(st, stm, nodes, tags, rng, divide);
+  if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 16) launch_count2c_cap<256 * 16, 0, true>(st, stm, nodes, tags, rng, divide);
+  else launch_count2c_cap<256 * 24, 0, true>(st, stm, nodes, tags, rng, divide);
 }
 
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,

@@ -160,6 +160,116 @@ __device__ __forceinline__ u32 ref_pawn_count_child(const Board& b, int f, int t
   return pc(push1) + pc(push2) + pc(and3(sh<PD::CW>(P), kNotH, enemy_c)) + pc(and3(sh<PD::CE>(P), kNotA, enemy_c));
 }
 
+// ------------------------------------------------ bulk split (k_count2c)
+// Pawn-sensitive squares of SIDE in `b` and SIDE's pawn-move count there.
+// For a quiet move f -> t of the other side (t empty, nothing captured), the
+// change in SIDE's pawn-move count is g(t) - g(f) (+1 correction when f, t are
+// the mid and landing squares of one double push), where
+//   g(x) = #SIDE pawns attacking x - [x is a push square of a SIDE pawn]
+//          - [x is the mid square of a double push whose landing is empty]
+//          - [x is the landing square of a double push whose mid is empty]
+// (derivation: DESIGN.md §3).  g vanishes outside
+//   G = pawn attacks | push squares | double-push landings with empty mid,
+// (mid squares are push squares), so a quiet move with f, t outside G leaves
+// SIDE's pawn count unchanged -- and the correction case has t or f on a mid
+// square, inside G.
+template <int SIDE>
+__device__ __forceinline__ u64 ref_pawn_sensitive(const Board& b, u32& pawn_cnt) {
+  typedef PawnDir<SIDE> PD;
+  const Sides s = sides<SIDE>(b);
+  const u64 q1 = sh<PD::F>(s.P);
+  const u64 cw = sh<PD::CW>(s.P) & kNotH, ce = sh<PD::CE>(s.P) & kNotA;
+  const u64 push1 = q1 & s.empty;
+  const u64 land = sh<PD::F>(push1) & PD::ROW_DBL;  // landings whose mid is empty
+  pawn_cnt = pc(push1) + pc(land & s.empty) + pc(cw & s.enemy) + pc(ce & s.enemy);
+  return bop3<0xFE>(q1, cw, ce) | land;
+}
+
+// Moves of STM in `b` with source in Fs and target in Ts ("simple" moves;
+// Ts holds empty squares only, so pawn captures never count): ref_count<STM>
+// with the sources and targets restricted.  Slider targets of sources in Fs
+// are the fill from (sliders & Fs): a target whose nearest slider behind it is
+// outside Fs is shadowed by that slider.
+template <int STM>
+__device__ __forceinline__ u32 ref_count_simple(const Board& b, u64 Fs, u64 Ts) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 push1 = sh<PD::F>(s.P & Fs) & s.empty;
+  u32 c = pc(push1 & Ts) + pc(and3(sh<PD::F>(push1), PD::ROW_DBL, Ts));
+  const u64 n = s.N & Fs;
+  c += pc(and3(sh<17>(n), kNotA, Ts)) + pc(and3(sh<15>(n), kNotH, Ts));
+  c += pc(and3(sh<10>(n), kNotAB, Ts)) + pc(and3(sh<6>(n), kNotGH, Ts));
+  c += pc(and3(sh<-6>(n), kNotAB, Ts)) + pc(and3(sh<-10>(n), kNotGH, Ts));
+  c += pc(and3(sh<-15>(n), kNotA, Ts)) + pc(and3(sh<-17>(n), kNotH, Ts));
+  c += king_moves(s.K & Fs, Ts);
+  const u64 e = s.empty, o = s.O & Fs, d = s.D & Fs;
+  c += pc(ray_attacks<8, kAll>(o, e) & Ts) + pc(ray_attacks<-8, kAll>(o, e) & Ts);
+  c += pc(ray_moves<1, kNotA>(o, e, Ts)) + pc(ray_moves<-1, kNotH>(o, e, Ts));
+  c += pc(ray_moves<9, kNotA>(d, e, Ts)) + pc(ray_moves<-9, kNotH>(d, e, Ts));
+  c += pc(ray_moves<7, kNotH>(d, e, Ts)) + pc(ray_moves<-7, kNotA>(d, e, Ts));
+  return c;
+}
+
+// ref_for_each_move<STM> without the simple moves (source in Fs, target in
+// Ts): leaper and pawn classes drop them set-wise before the bit loop (the
+// source of target t is t - delta), slider classes per move once the source
+// is known.
+template <int STM, class Visit>
+__device__ __forceinline__ void ref_for_each_special(const Board& b, u64 Fs, u64 Ts, Visit&& visit) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 no = s.notown, e = s.empty;
+  auto leap = [&](u64 targets, int delta, u64 simple) {
+    targets &= ~simple;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(t - delta, t);
+    }
+  };
+  const u64 push1 = sh<PD::F>(s.P) & e;
+  leap(push1, PD::F, sh<PD::F>(Fs) & Ts);
+  leap(sh<PD::F>(push1 & PD::ROW_AFTER1) & e, 2 * PD::F, sh<2 * PD::F>(Fs) & Ts);
+  leap(sh<PD::CW>(s.P & kNotA) & s.enemy, PD::CW, 0);
+  leap(sh<PD::CE>(s.P & kNotH) & s.enemy, PD::CE, 0);
+  const u64 n = s.N;
+  leap(sh<17>(n & kNotH) & no, 17, sh<17>(Fs) & Ts);
+  leap(sh<15>(n & kNotA) & no, 15, sh<15>(Fs) & Ts);
+  leap(sh<10>(n & kNotGH) & no, 10, sh<10>(Fs) & Ts);
+  leap(sh<6>(n & kNotAB) & no, 6, sh<6>(Fs) & Ts);
+  leap(sh<-6>(n & kNotGH) & no, -6, sh<-6>(Fs) & Ts);
+  leap(sh<-10>(n & kNotAB) & no, -10, sh<-10>(Fs) & Ts);
+  leap(sh<-15>(n & kNotH) & no, -15, sh<-15>(Fs) & Ts);
+  leap(sh<-17>(n & kNotA) & no, -17, sh<-17>(Fs) & Ts);
+  const u64 k = s.K;
+  leap(sh<8>(k) & no, 8, sh<8>(Fs) & Ts);
+  leap(sh<-8>(k) & no, -8, sh<-8>(Fs) & Ts);
+  leap(sh<1>(k & kNotH) & no, 1, sh<1>(Fs) & Ts);
+  leap(sh<-1>(k & kNotA) & no, -1, sh<-1>(Fs) & Ts);
+  leap(sh<9>(k & kNotH) & no, 9, sh<9>(Fs) & Ts);
+  leap(sh<7>(k & kNotA) & no, 7, sh<7>(Fs) & Ts);
+  leap(sh<-7>(k & kNotH) & no, -7, sh<-7>(Fs) & Ts);
+  leap(sh<-9>(k & kNotA) & no, -9, sh<-9>(Fs) & Ts);
+  auto slide = [&](u64 targets, auto dtag) {
+    constexpr int D = decltype(dtag)::value;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      const int f = slider_source<D>(s.occ, t);
+      if (((Fs >> f) & (Ts >> t) & 1) == 0) visit(f, t);
+    }
+  };
+  using std::integral_constant;
+  slide(ray_attacks<8, kAll>(s.O, e) & no, integral_constant<int, 0>{});
+  slide(ray_attacks<-8, kAll>(s.O, e) & no, integral_constant<int, 1>{});
+  slide(ray_attacks<1, kNotA>(s.O, e) & no, integral_constant<int, 2>{});
+  slide(ray_attacks<-1, kNotH>(s.O, e) & no, integral_constant<int, 3>{});
+  slide(ray_attacks<9, kNotA>(s.D, e) & no, integral_constant<int, 4>{});
+  slide(ray_attacks<-9, kNotH>(s.D, e) & no, integral_constant<int, 5>{});
+  slide(ray_attacks<7, kNotH>(s.D, e) & no, integral_constant<int, 6>{});
+  slide(ray_attacks<-7, kNotA>(s.D, e) & no, integral_constant<int, 7>{});
+}
+
 // Runtime side-to-move version.
 __device__ __forceinline__ u32 ref_count_rt(const Board& b, u32 stm) {
   return stm ? ref_count<1>(b) : ref_count<0>(b);
