@@ -654,7 +654,7 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       qn = __builtin_amdgcn_readfirstlane(qn - 64);
     };
     if constexpr (BULK) add(tid, (u32)simple_leaves, valid);
-    if constexpr (PHASE != 0) acc += cnt + base + (u32)att;
+    if constexpr (PHASE == 1 || PHASE == 2) acc += cnt + base + (u32)att;
     for (u32 wbase = 0; wbase < (PHASE == 2 ? 0u : total); wbase += CAP) {
       if (wbase) __syncthreads();  // previous window fully read
       // each (f, t) of this parent's enumerated (BULK: special) moves -> visit(f, t)
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       __syncthreads();
       const u32 nslots = min(CAP, total - wbase);
       // two slots per lane per step, loaded together, so the LDS round trips overlap
-      u32 r0 = PHASE ? nslots : w * 64;
+      u32 r0 = (PHASE == 1 || PHASE == 2) ? nslots : w * 64;
       for (; r0 + 256 < nslots; r0 += 512) {
         const u32 ra = r0 + lane, rb = r0 + 256 + lane;
         const bool lb = rb < nslots;
@@ -806,7 +806,7 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
 }
 
 // Final-stage selection (for A/B measurement): DC_FINAL=2b forces k_count2b
-// under REF; DC_C2C_CAP=20|24|28 sets k_count2c's child slots per parent.
+// under REF (k_count2c: 24 child slots per parent, the best of 20/24/28).
 static int final_variant() {
   static const int v = [] {
     const char* e = std::getenv("DC_FINAL");
@@ -837,7 +837,6 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
   if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 16) launch_count2c_cap<256 * 16, 0, true>(st, stm, nodes, tags, rng, divide);
   else launch_count2c_cap<256 * 24, 0, true>(st, stm, nodes, tags, rng, divide);
 }
 

@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 O=gpurun_out; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "perft or replica" > $O/ab_pytest.log 2>&1 || { tail -30 $O/ab_pytest.log; exit 1; }
 tail -2 $O/ab_pytest.log
-for v in "DC_FINAL=2b" "DC_C2C_CAP=20" "DC_C2C_CAP=24" "DC_C2C_CAP=28"; do
+for v in ${AB_VARIANTS:-"DC_FINAL=2b" "DC_C2C_PHASE=3" "DC_C2C_PHASE=0"}; do
   env $v timeout -k 10 120 python -u bench.py --no-cpu --no-replay --steps 20 > $O/ab_$v.json 2> $O/ab_err.log || { cat $O/ab_err.log; exit 2; }
   python - "$v" <<'PY'
 import json, sys
