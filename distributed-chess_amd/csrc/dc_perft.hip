@@ -592,17 +592,18 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
     if (valid) {
       p = load_board(nodes, i);
       tag = tags[i];
-      cnt = ref_count<STM>(p);
-      base = ref_count_nonpawn<1 - STM>(p, att);
       if constexpr (BULK) {
-        u32 pawn_o = 0;
-        const u64 keep = ~(att | ref_pawn_sensitive<1 - STM>(p, pawn_o));
-        const Sides sd = sides<STM>(p);
-        Fs = sd.own & keep;
-        Ts = sd.empty & keep;
-        const u32 n_simple = ref_count_simple<STM>(p, Fs, Ts);
-        cnt -= n_simple;  // enumerated (special) children only
-        simple_leaves = (u64)n_simple * (base + pawn_o);
+        ParentSplit ps;
+        ref_parent_split<STM>(p, ps);
+        base = ps.base;
+        att = ps.att;
+        Fs = ps.Fs;
+        Ts = ps.Ts;
+        cnt = ps.n_total - ps.n_simple;  // enumerated (special) children only
+        simple_leaves = (u64)ps.n_simple * (ps.base + ps.pawn_o);
+      } else {
+        cnt = ref_count<STM>(p);
+        base = ref_count_nonpawn<1 - STM>(p, att);
       }
     }
     u64 total64;

@@ -210,6 +210,91 @@ __device__ __forceinline__ u32 ref_count_simple(const Board& b, u64 Fs, u64 Ts) 
   return c;
 }
 
+// Two occluded fills toward S sharing the propagator masks (one pass per
+// direction keeps few masks live; see ref_parent_split).
+template <int S, u64 M>
+__device__ __forceinline__ void ray_attacks2(u64 g1, u64 g2, u64 empty, u64& r1, u64& r2) {
+  u64 pro = empty & M;
+  g1 = or_and(g1, pro, sh<S>(g1));
+  g2 = or_and(g2, pro, sh<S>(g2));
+  pro &= sh<S>(pro);
+  g1 = or_and(g1, pro, sh<2 * S>(g1));
+  g2 = or_and(g2, pro, sh<2 * S>(g2));
+  pro &= sh<2 * S>(pro);
+  g1 = or_and(g1, pro, sh<4 * S>(g1));
+  g2 = or_and(g2, pro, sh<4 * S>(g2));
+  r1 = sh<S>(g1) & M;
+  r2 = sh<S>(g2) & M;
+}
+
+// Everything k_count2c needs per parent P (side STM to move, opponent O):
+//   base, att = ref_count_nonpawn<O>;  pawn_o (and G) = ref_pawn_sensitive<O>;
+//   Fs = own & ~(att | G), Ts = empty & ~(att | G);
+//   n_total = ref_count<STM>, n_simple = ref_count_simple<STM>(Fs, Ts),
+// with STM's all-source and Fs-source fills fused per direction.  Computed
+// as four separate functions, the compiler kept every direction's fill masks
+// live across them (CSE) and spilled 184 B per lane -- 0.9 GB of scratch
+// traffic per perft(7) launch (rocprofv3 FETCH_SIZE).
+struct ParentSplit {
+  u64 att, Fs, Ts;
+  u32 base, pawn_o, n_total, n_simple;
+};
+
+template <int STM>
+__device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r) {
+  r.base = ref_count_nonpawn<1 - STM>(b, r.att);
+  const u64 keep = ~(r.att | ref_pawn_sensitive<1 - STM>(b, r.pawn_o));
+  const Sides s = sides<STM>(b);
+  const u64 Fs = s.own & keep, Ts = s.empty & keep, no = s.notown;
+  r.Fs = Fs;
+  r.Ts = Ts;
+  u64 e = s.empty;
+  asm volatile("" : "+v"(e));  // opaque copy: no reuse of the opponent's fill masks
+  typedef PawnDir<STM> PD;
+  const u64 push1 = sh<PD::F>(s.P) & e, push1s = sh<PD::F>(s.P & Fs) & e;
+  u32 t = pc(push1) + pc(and3(sh<PD::F>(push1), PD::ROW_DBL, e));
+  u32 m = pc(push1s & Ts) + pc(and3(sh<PD::F>(push1s), PD::ROW_DBL, Ts));
+  t += pc(and3(sh<PD::CW>(s.P), kNotH, s.enemy)) + pc(and3(sh<PD::CE>(s.P), kNotA, s.enemy));
+  const u64 n = s.N, ns = s.N & Fs;
+  auto leap = [&](auto dtag, u64 guard) {
+    constexpr int D = decltype(dtag)::value;
+    t += pc(and3(sh<D>(n), guard, no));
+    m += pc(and3(sh<D>(ns), guard, Ts));
+  };
+  using std::integral_constant;
+  leap(integral_constant<int, 17>{}, kNotA);
+  leap(integral_constant<int, 15>{}, kNotH);
+  leap(integral_constant<int, 10>{}, kNotAB);
+  leap(integral_constant<int, 6>{}, kNotGH);
+  leap(integral_constant<int, -6>{}, kNotAB);
+  leap(integral_constant<int, -10>{}, kNotGH);
+  leap(integral_constant<int, -15>{}, kNotA);
+  leap(integral_constant<int, -17>{}, kNotH);
+  t += king_moves(s.K, no);
+  m += king_moves(s.K & Fs, Ts);
+  auto slide = [&](u64 sl, auto stag, auto mtag) {
+    constexpr int S = decltype(stag)::value;
+    constexpr u64 M = decltype(mtag)::value;
+    u64 ra, rs;
+    ray_attacks2<S, M>(sl, sl & Fs, e, ra, rs);
+    t += pc(ra & no);
+    m += pc(rs & Ts);
+  };
+  using K = std::integral_constant<u64, kAll>;
+  using NA = std::integral_constant<u64, kNotA>;
+  using NH = std::integral_constant<u64, kNotH>;
+  slide(s.O, integral_constant<int, 8>{}, K{});
+  slide(s.O, integral_constant<int, -8>{}, K{});
+  slide(s.O, integral_constant<int, 1>{}, NA{});
+  slide(s.O, integral_constant<int, -1>{}, NH{});
+  slide(s.D, integral_constant<int, 9>{}, NA{});
+  slide(s.D, integral_constant<int, -9>{}, NH{});
+  slide(s.D, integral_constant<int, 7>{}, NH{});
+  slide(s.D, integral_constant<int, -7>{}, NA{});
+  r.n_total = t;
+  r.n_simple = m;
+}
+
 // ref_for_each_move<STM> without the simple moves (source in Fs, target in
 // Ts): leaper and pawn classes drop them set-wise before the bit loop (the
 // source of target t is t - delta), slider classes per move once the source
