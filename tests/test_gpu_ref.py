@@ -211,6 +211,60 @@ def test_replay_edge_cases(engine):
     assert (bm == fbm).all() and (dg == fdg).all() and st["validated"] == int(fst[0])
 
 
+def _replay_from(start, n_games, n_plies, seed):
+    """Seeded games from `start` and their expected replay, move by move through
+    the literal restatement (refcpu validate_move, chess.rs:82-125; apply as
+    chess.rs:72-77).  Mix: legal moves, random 12-bit words, OOR words, and
+    games that end early (sentinel rest)."""
+    rng = np.random.default_rng(seed)
+    mv = np.full((n_plies, n_games), O.SENTINEL, np.uint16)
+    bm = np.zeros((n_plies, (n_games + 63) // 64), np.uint64)
+    dg = np.zeros(n_games, np.uint64)
+    validated = accepted = 0
+    for g in range(n_games):
+        cells, stm = start.cells.copy(), start.stm
+        end = n_plies if rng.random() < 0.8 else int(rng.integers(0, n_plies + 1))
+        for ply in range(end):
+            r = rng.random()
+            legal = O.fast_gen_moves(O.Pos(cells, stm))
+            if r < 0.6 and len(legal):
+                m = int(rng.choice(legal))
+            elif r < 0.95:
+                m = int(rng.integers(0, 4096))
+            else:
+                m = 0x8000 | int(rng.integers(0, 0x7FFF))
+            mv[ply, g] = m
+            validated += 1
+            f, t = m & 63, (m >> 6) & 63
+            if m & 0x8000 or O.ref_validate(cells, stm, f >> 3, f & 7, t >> 3, t & 7) != O.OK:
+                continue
+            cells[t], cells[f] = cells[f], -1
+            stm ^= 1
+            accepted += 1
+            bm[ply, g >> 6] |= np.uint64(1 << (g & 63))
+        dg[g] = O.digest(cells, stm)
+    return mv, bm, dg, validated, accepted
+
+
+@pytest.mark.parametrize("kind", ["midgame_black", "odd_pieces"])
+def test_replay_from_custom_start_vs_refcpu(engine, kind):
+    """dc_replay with start != NULL (the LDS-mailbox kernel packs it on the host)."""
+    if kind == "midgame_black":
+        start = _positions(1, 44)[0]
+        start.stm = 1
+    else:
+        rng = np.random.default_rng(9)
+        cells = np.full(64, -1, np.int8)
+        sq = rng.choice(64, 26, replace=False)
+        cells[sq] = rng.integers(0, 2, 26) * 8 + rng.integers(0, 7, 26)  # includes kind 6 (OTHER)
+        start = O.Pos(cells, 1, 0, -1)
+    mv, bm, dg, validated, accepted = _replay_from(start, 100, 37, 5)
+    gbm, gdg, st = engine.replay(mv, start=pos_of(start))
+    assert (gbm == bm).all() and (gdg == dg).all()
+    assert st["validated"] == validated and st["accepted"] == accepted
+    assert st["digest_xor"] == int(np.bitwise_xor.reduce(dg))
+
+
 def test_replay_vs_refcpu_sample(engine):
     mv = engine.gen_games(0x5EED20241022, 123456, 512, 80, 32)
     bm, dg, st = engine.replay(mv)
