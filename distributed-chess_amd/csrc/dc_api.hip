@@ -9,6 +9,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -29,12 +31,17 @@ using dc::u64;
 static_assert(sizeof(dc_pos) == sizeof(DevPos), "dc_pos / DevPos layout");
 
 // ------------------------------------------------------------------ buffers
+// Bumped whenever any device buffer moves: captured perft graphs hold raw
+// pointers and are re-captured after a bump.
+static std::atomic<uint64_t> g_alloc_epoch{0};
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
+    g_alloc_epoch.fetch_add(1);
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
@@ -89,6 +96,16 @@ struct dc_ctx {
   DBuf<Board> root;
   DBuf<uint16_t> root_meta;
   dc::PerftResult* res_host = nullptr;  // pinned
+  // The last perft launch sequence, captured as a hipGraph (see perft_run).
+  struct PerftKey {
+    u32 rules, depth, split, shard, n_shards, stm;
+    uint64_t epoch;
+    bool operator==(const PerftKey& o) const {
+      return rules == o.rules && depth == o.depth && split == o.split && shard == o.shard &&
+             n_shards == o.n_shards && stm == o.stm && epoch == o.epoch;
+    }
+  } pkey{};
+  hipGraphExec_t pgraph = nullptr;
   struct RootStage {
     Board b;
     uint16_t meta;
@@ -108,6 +125,7 @@ struct dc_ctx {
     res.release();
     rng.release();
     desc.release();
+    if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (res_host) (void)hipHostFree(res_host);
     if (root_host) (void)hipHostFree(root_host);
     pos.release();
@@ -581,8 +599,12 @@ int read_range(dc_ctx* c, int level, u64* n) {
   return DC_SUCCESS;
 }
 
-int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
-              uint32_t n_shards, bool exact, dc::PerftResult* out) {
+// Enqueues one perft on the context stream up to (not including) the result
+// copy.  *host_sync is set when a level size had to be read back on the host
+// (exact mode or a level beyond the speculative budget): such a sequence
+// depends on data and is never captured as a graph.
+int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
+                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync) {
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   const u32 F = depth >= 3 ? depth - 2 : 1;       // level handed to the final stage
@@ -645,6 +667,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
   while (L < F) {
     const int stm = pos->stm ^ (L & 1);
     if (exact || nb * kBranchBound * kNodeBytes > kSpecBudget) {
+      *host_sync = true;
       e = read_range(c, L, &nb);
       if (e != DC_SUCCESS) return e;
     }
@@ -653,6 +676,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
     e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0);
     if (e != DC_SUCCESS) return e;
     if (exact_next) {
+      *host_sync = true;
       e = read_range(c, L + 1, &cap_next);
       if (e != DC_SUCCESS) return e;
       if (cap_next > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
@@ -677,10 +701,69 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
                               c->tags[buf].p, c->rng.p + L, nb, c->res.p->divide, nullptr);
     }));
   }
+  return DC_SUCCESS;
+}
+
+// DC_GRAPH=0 disables the perft graph (A/B).
+static bool perft_graphs_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("DC_GRAPH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// One perft.  A repeated configuration (same rules, depth, shard, side to move
+// and buffers) replays the launch sequence captured from its previous run as a
+// hipGraph: the 12 stream operations of a perft(7) go to the GPU as one launch,
+// which removes the per-kernel launch gaps.  The root position
+// is read from the pinned staging block when the graph runs.
+int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
+              uint32_t n_shards, bool exact, dc::PerftResult* out) {
+  const bool graphable = !exact && !c->profiling && perft_graphs_enabled();
+  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
+  if (graphable && c->pgraph && c->pkey == key) {
+    c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
+    c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
+    HIP_TRY(hipGraphLaunch(c->pgraph, c->stream));
+    int e = sync_ctx(c);
+    if (e != DC_SUCCESS) return e;
+    *out = *c->res_host;
+    return DC_SUCCESS;
+  }
+  bool host_sync = false;
+  int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, exact, &host_sync);
+  if (e != DC_SUCCESS) return e;
   HIP_TRY(hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream));
   e = sync_ctx(c);
   if (e != DC_SUCCESS) return e;
   *out = *c->res_host;
+  if (!graphable || host_sync || out->overflow) return DC_SUCCESS;
+  // capture the same sequence for the next call (best effort: any failure
+  // leaves the plain path in place)
+  if (c->pgraph) {
+    (void)hipGraphExecDestroy(c->pgraph);
+    c->pgraph = nullptr;
+  }
+  if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) {
+    (void)hipGetLastError();
+    return DC_SUCCESS;
+  }
+  bool hs = false;
+  int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs);
+  if (ce == DC_SUCCESS &&
+      hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
+    ce = DC_EHIP;
+  hipGraph_t g = nullptr;
+  const hipError_t ee = hipStreamEndCapture(c->stream, &g);
+  if (ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
+      hipGraphInstantiate(&c->pgraph, g, nullptr, nullptr, 0) == hipSuccess) {
+    c->pkey = key;
+  } else {
+    c->pgraph = nullptr;
+  }
+  if (g) (void)hipGraphDestroy(g);
+  (void)hipGetLastError();
   return DC_SUCCESS;
 }
 
