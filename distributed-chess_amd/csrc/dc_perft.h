@@ -15,8 +15,8 @@ struct PerftResult {
   uint16_t root_moves[256];
   u32 n_root;
   u32 overflow;
-  u32 path;  // final stage: 0 descriptor list, 1 LDS count2
-  u32 pad;
+  u32 path;        // final stage: 0 descriptor list, 1 LDS count2
+  u32 next_chunk;  // k_count2c's dynamic chunk counter (zeroed with the block)
   u64 level_n[16];
 };
 

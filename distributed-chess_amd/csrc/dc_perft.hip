@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restric
 // compacted into LDS slots at block-scan offsets, then every lane makes one
 // child per round and stores it at chunk_base + slot -- consecutive lanes write
 // consecutive nodes (coalesced), and a ~200k-node ply keeps all lanes busy.
-constexpr u32 kWriteCap = 256 * 24;
+constexpr u32 kWriteCap = 256 * 30;  // ply-5 chunks of perft(7) average 24.8 children per parent: one window
 
 struct WriteShared {
   Board par[256];
@@ -555,6 +555,7 @@ struct C2cShared {
   u32 queue[4][kC2cQueue];
   u64 hist[256];
   u64 wsum[4];
+  u32 next;
   uint16_t ptag[256];
 };
 
@@ -575,17 +576,23 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
 // 2 also skips the enumeration, leaving the per-parent counts.
 template <int STM, u32 CAP, int PHASE = 0, bool BULK = true>
 __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
-                                                 const Range* __restrict__ rng, u64* __restrict__ divide) {
+                                                 const Range* __restrict__ rng, u64* __restrict__ divide,
+                                                 u32* __restrict__ next_chunk) {
   __shared__ C2cShared<CAP> sh;
   tag_hist_init(sh.hist);
   const u32 tid = threadIdx.x, w = tid >> 6, lane = lane_id();
   u32* q = sh.queue[w];
   const u64 lo = rng->lo, hi = rng->hi;
-  const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;
-  const u64 blo = min(hi, lo + (u64)blockIdx.x * per), bhi = min(hi, blo + per);
-  for (u64 s = blo; s < bhi; s += kChunk) {
+  // Blocks take 256-parent chunks from a counter: the cost of a chunk varies
+  // with its positions, and static ranges left the slowest block behind (a
+  // sharded launch has only ~3 chunks per block).
+  for (;;) {
+    if (tid == 0) sh.next = atomicAdd(next_chunk, 1u);
+    __syncthreads();
+    const u64 s = lo + (u64)sh.next * kChunk;
+    if (s >= hi) break;  // block-uniform
     const u64 i = s + tid;
-    const bool valid = i < bhi;
+    const bool valid = i < hi;
     Board p{0, 0, 0, 0};
     u32 tag = 0, cnt = 0, base = 0;
     u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
@@ -819,12 +826,17 @@ static int final_variant() {
 template <u32 CAP, int PHASE, bool BULK>
 static void launch_count2c_cap(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
                                u64* divide) {
+  // divide is the first member of the run's PerftResult (perft_enqueue): its
+  // next_chunk field, zeroed with the block at the start of the run, is the
+  // chunk counter
+  static_assert(offsetof(PerftResult, divide) == 0, "divide heads PerftResult");
+  u32* next = &reinterpret_cast<PerftResult*>(divide)->next_chunk;
   if (stm) {
     auto k = k_count2c<1, CAP, PHASE, BULK>;
-    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide);
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide, next);
   } else {
     auto k = k_count2c<0, CAP, PHASE, BULK>;
-    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide);
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide, next);
   }
 }
 
