@@ -599,6 +599,14 @@ int read_range(dc_ctx* c, int level, u64* n) {
   return DC_SUCCESS;
 }
 
+static bool shard_contiguous() {
+  static const bool v = [] {
+    const char* e = std::getenv("DC_SHARD");
+    return e && std::strcmp(e, "contig") == 0;
+  }();
+  return v;
+}
+
 // Enqueues one perft on the context stream up to (not including) the result
 // copy.  *host_sync is set when a level size had to be read back on the host
 // (exact mode or a level beyond the speculative budget): such a sequence
@@ -647,7 +655,24 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   u32 L = T;
   u64 nb = cap_T;
   int buf = 0;
-  if (sharded && L == S) HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
+  // This rank's shard of level S: strided (default) or contiguous (DC_SHARD=contig).
+  auto take_shard = [&]() -> int {
+    if (shard_contiguous()) {
+      HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
+      return DC_SUCCESS;
+    }
+    int e2 = ensure_level(c, buf ^ 1, nb, fide);
+    if (e2 != DC_SUCCESS) return e2;
+    HIP_TRY(dc::launch_gather_shard(c->stream, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr, c->tags[buf].p,
+                                    c->rng.p + L, shard, n_shards, c->nodes[buf ^ 1].p,
+                                    fide ? c->meta[buf ^ 1].p : nullptr, c->tags[buf ^ 1].p));
+    buf ^= 1;
+    return DC_SUCCESS;
+  };
+  if (sharded && L == S) {
+    e = take_shard();
+    if (e != DC_SUCCESS) return e;
+  }
   // One level: counts + chunk sums, chunk scan into Range L+1 (capacity cap), then `write`.
   auto count_and_scan = [&](int stm, u64 cap, int select_path) -> int {
     const u64 nch = std::max<u64>(dc::chunks_for(nb), 1);
@@ -692,7 +717,10 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     buf ^= 1;
     ++L;
     nb = cap_next;
-    if (sharded && L == S) HIP_TRY(dc::launch_slice(c->stream, c->rng.p + L, shard, n_shards));
+    if (sharded && L == S) {
+      e = take_shard();
+      if (e != DC_SUCCESS) return e;
+    }
   }
   const int stm = pos->stm ^ (L & 1);
   if (depth >= 2) {

@@ -41,6 +41,10 @@ hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* n
                               const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
                               const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap);
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
+// Strided shard: every n_shards-th node of the level, gathered to out[0..).
+hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* in_meta, const uint16_t* in_tags,
+                               Range* rng, u32 shard, u32 n_shards, Board* out, uint16_t* out_meta,
+                               uint16_t* out_tags);
 // plies = 1 (k_count1) or 2: the fused last two plies through LDS, k_count2b
 // (256-parent blocks; res == nullptr) or the wave-level k_count2 (runs only
 // when res->path == 1).

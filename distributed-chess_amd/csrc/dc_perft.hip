@@ -357,6 +357,27 @@ __global__ void k_slice(Range* rng, u32 shard, u32 n_shards) {
   *rng = Range{lo + n * shard / n_shards, lo + n * (shard + 1) / n_shards};
 }
 
+// Strided shard of a level: nodes lo + shard, lo + shard + n_shards, ... are
+// gathered to the front of `out` and the level's Range becomes [0, count).
+// Subtree sizes vary along the frontier (a contiguous eighth of ply 3 held
+// 1.5x the leaves of another); every n-th node evens them out.  One block:
+// all threads read the Range before thread 0 rewrites it.
+__global__ __launch_bounds__(1024) void k_gather_shard(const Board* __restrict__ in, const uint16_t* __restrict__ in_meta,
+                                                       const uint16_t* __restrict__ in_tags, Range* rng, u32 shard,
+                                                       u32 n_shards, Board* __restrict__ out,
+                                                       uint16_t* __restrict__ out_meta, uint16_t* __restrict__ out_tags) {
+  const u64 lo = rng->lo, hi = rng->hi;
+  const u64 n = hi > lo + shard ? (hi - lo - shard + n_shards - 1) / n_shards : 0;
+  for (u64 k = threadIdx.x; k < n; k += blockDim.x) {
+    const u64 i = lo + shard + k * n_shards;
+    store_board(out, k, load_board(in, i));
+    if (in_meta) out_meta[k] = in_meta[i];
+    out_tags[k] = in_tags[i];
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) *rng = Range{0, n};
+}
+
 template <class R, int STM>
 __global__ __launch_bounds__(256) void k_count1(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                 const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
@@ -805,6 +826,14 @@ hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* n
                               const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap) {
   DC_LAUNCH_RULES_STM(k_level_write, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, counts, chunk_base,
                       out, out_meta, out_tags, cap);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* in_meta, const uint16_t* in_tags,
+                               Range* rng, u32 shard, u32 n_shards, Board* out, uint16_t* out_meta,
+                               uint16_t* out_tags) {
+  hipLaunchKernelGGL(k_gather_shard, dim3(1), dim3(1024), 0, st, in, in_meta, in_tags, rng, shard, n_shards, out,
+                     out_meta, out_tags);
   return hipGetLastError();
 }
 
