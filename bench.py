@@ -318,7 +318,7 @@ def main():
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic (startpos tree; seeded random-legal games for replay)",
         "config": {"workload": f"perft(startpos, {args.depth}) RULES_REF (bit-exact with core/src/chess.rs), "
-                               f"frontier split at ply {args.split} into contiguous shards over ranks, "
+                               f"frontier split at ply {args.split} into strided shards over ranks, "
                                "per-root-move counts all-reduced over RCCL",
                    "depth": args.depth, "rules": "REF", "leaves_per_step": REF_STARTPOS.get(args.depth),
                    "parallelism": f"dp{d.world}"},
