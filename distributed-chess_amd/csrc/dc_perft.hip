@@ -617,6 +617,7 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
     Board p{0, 0, 0, 0};
     u32 tag = 0, cnt = 0, base = 0;
     u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
+    u32 nsim = 0;
     if (valid) {
       p = load_board(nodes, i);
       tag = tags[i];
@@ -629,6 +630,7 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
         Ts = ps.Ts;
         cnt = ps.n_total - ps.n_simple;  // enumerated (special) children only
         simple_leaves = (u64)ps.n_simple * (ps.base + ps.pawn_o);
+        nsim = ps.n_simple;
       } else {
         cnt = ref_count<STM>(p);
         base = ref_count_nonpawn<1 - STM>(p, att);
@@ -645,6 +647,7 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
     const u32 tag0 = sh.ptag[0];
     u64 acc = 0;  // grandchildren under parents whose tag == tag0
     auto add = [&](u32 pl, u32 k, bool live) {
+      if constexpr (PHASE == 7) return;
       if (!live) return;
       const u32 ptag = sh.ptag[pl];
       if (ptag == tag0) acc += k;
@@ -671,6 +674,13 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       if (live && quiet) add(pl, c.base + ref_pawn_count_child<1 - STM>(c.pb, f, t), true);
       const bool full = live && !quiet;
       const u64 em = ballot(full);
+      if constexpr (PHASE == 7) {  // statistics: divide[0] quiet special children, [1] full-recount children
+        const u64 qm = ballot(live && quiet);
+        if (lane == 0) {
+          atomicAdd((unsigned long long*)divide, (unsigned long long)__popcll(qm));
+          atomicAdd((unsigned long long*)(divide + 1), (unsigned long long)__popcll(em));
+        }
+      }
       if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
       qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
     };
@@ -682,7 +692,14 @@ __global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ no
       if (lane + 64 < qn) q[lane] = q[lane + 64];
       qn = __builtin_amdgcn_readfirstlane(qn - 64);
     };
-    if constexpr (BULK) add(tid, (u32)simple_leaves, valid);
+    if constexpr (BULK && PHASE != 7) add(tid, (u32)simple_leaves, valid);
+    if constexpr (PHASE == 7) {  // [2] simple children, [3] parents
+      const u64 ns = wave_sum64(nsim), np = __popcll(ballot(valid));
+      if (lane == 0) {
+        atomicAdd((unsigned long long*)(divide + 2), (unsigned long long)ns);
+        atomicAdd((unsigned long long*)(divide + 3), (unsigned long long)np);
+      }
+    }
     if constexpr (PHASE == 1 || PHASE == 2) acc += cnt + base + (u32)att;
     for (u32 wbase = 0; wbase < (PHASE == 2 ? 0u : total); wbase += CAP) {
       if (wbase) __syncthreads();  // previous window fully read
@@ -879,6 +896,7 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
   if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 7) launch_count2c_cap<256 * 24, 7, true>(st, stm, nodes, tags, rng, divide);
   else launch_count2c_cap<256 * 24, 0, true>(st, stm, nodes, tags, rng, divide);
 }
 
