@@ -20,6 +20,8 @@
 
 #include "../../include/dchess.h"
 #include "dc_fide.h"
+#include "dc_hash.h"
+#include "dc_keccak.h"
 #include "dc_kernels.h"
 #include "dc_perft.h"
 
@@ -114,6 +116,9 @@ struct dc_ctx {
   DBuf<DevPos> pos;
   DBuf<uint16_t> moves;
   DBuf<uint8_t> verdicts, info;
+  DBuf<char> hash_text;    // escaped names + start history of dc_state_hash*
+  DBuf<u32> hash_off;
+  DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
 
   ~dc_ctx() {
@@ -131,6 +136,9 @@ struct dc_ctx {
     pos.release();
     verdicts.release();
     info.release();
+    hash_text.release();
+    hash_off.release();
+    hashes.release();
     bitmap.release();
     digests.release();
     stats5.release();
@@ -537,6 +545,141 @@ int dc_replay(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* mo
     HIP_TRY(hipMemcpyAsync(bitmap, c->bitmap.p, words * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
   if (digests && n_games)
     HIP_TRY(hipMemcpyAsync(digests, c->digests.p, (size_t)n_games * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+// ------------------------------------------------------------ state hashes
+}  // extern "C"
+
+namespace {
+
+// serde_json's string escaping (serde_json 1.0 ser.rs ESCAPE table): '"' and
+// '\\', \b \t \n \f \r, other bytes < 0x20 as \u00xx (lowercase hex); every
+// other byte, UTF-8 included, verbatim.
+void json_escape(const char* s, size_t n, std::string& out) {
+  static const char hex[] = "0123456789abcdef";
+  for (size_t i = 0; i < n; ++i) {
+    const unsigned char ch = (unsigned char)s[i];
+    switch (ch) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\b': out += "\\b"; break;
+      case '\t': out += "\\t"; break;
+      case '\n': out += "\\n"; break;
+      case '\f': out += "\\f"; break;
+      case '\r': out += "\\r"; break;
+      default:
+        if (ch < 0x20) {
+          out += "\\u00";
+          out += hex[ch >> 4];
+          out += hex[ch & 15];
+        } else {
+          out += (char)ch;
+        }
+    }
+  }
+}
+
+// Rust's str::split_whitespace().count() (char::is_whitespace = Unicode White_Space).
+u32 count_ws_tokens(const char* s, size_t n) {
+  auto is_ws = [](u32 c) {
+    return (c >= 9 && c <= 13) || c == 32 || c == 0x85 || c == 0xA0 || c == 0x1680 || (c >= 0x2000 && c <= 0x200A) ||
+           c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+  };
+  u32 count = 0;
+  bool in_tok = false;
+  for (size_t i = 0; i < n;) {
+    const unsigned char b0 = (unsigned char)s[i];
+    u32 c = b0, len = 1;
+    if (b0 >= 0xF0) { c = b0 & 7; len = 4; }
+    else if (b0 >= 0xE0) { c = b0 & 15; len = 3; }
+    else if (b0 >= 0xC0) { c = b0 & 31; len = 2; }
+    for (u32 k = 1; k < len && i + k < n; ++k) c = (c << 6) | ((unsigned char)s[i + k] & 63);
+    i += len;
+    const bool ws = is_ws(c);
+    if (!ws && !in_tok) ++count;
+    in_tok = !ws;
+  }
+  return count;
+}
+
+// Stages the escaped names + start history on the device; returns the
+// history's JSON length and token count.
+int stage_hash_text(dc_ctx* c, const char* history, const char* names, const uint32_t* names_off, uint32_t n_games,
+                    u32* hist_len, u32* hist_tokens) {
+  const size_t hn = history ? std::strlen(history) : 0;
+  std::string text;
+  json_escape(history ? history : "", hn, text);
+  *hist_len = (u32)text.size();
+  *hist_tokens = count_ws_tokens(history ? history : "", hn);
+  std::vector<u32> off((size_t)2 * n_games + 1);
+  for (size_t i = 0; i < (size_t)2 * n_games; ++i) {
+    off[i] = (u32)text.size();
+    if (names_off[i + 1] < names_off[i]) return DC_EINVAL;
+    json_escape(names + names_off[i], names_off[i + 1] - names_off[i], text);
+    if (text.size() > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
+  }
+  off[(size_t)2 * n_games] = (u32)text.size();
+  HIP_TRY(c->hash_text.ensure(std::max<size_t>(text.size(), 1)));
+  HIP_TRY(c->hash_off.ensure(off.size()));
+  HIP_TRY(hipMemcpyAsync(c->hash_text.p, text.data(), text.size(), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->hash_off.p, off.data(), off.size() * sizeof(u32), hipMemcpyHostToDevice, c->stream));
+  return sync_ctx(c);  // text / off are host temporaries
+}
+
+int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const char* names,
+                    const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
+                    uint8_t* d_hashes) {
+  if (!names || !names_off || (n_games && n_plies && !d_moves) || (n_games && !d_hashes)) return DC_EINVAL;
+  dc_pos s0;
+  if (start) s0 = *start;
+  else dc_startpos(&s0);
+  if (s0.stm > 1) return DC_EINVAL;
+  // pieces of unknown kind keep a proto kind string this engine does not know
+  if (s0.bb[3] & ~(s0.bb[1] | s0.bb[2])) return DC_EUNSUPPORTED;
+  if (n_games == 0) return DC_SUCCESS;
+  u32 hist_len = 0, hist_tokens = 0;
+  int e = stage_hash_text(c, history, names, names_off, n_games, &hist_len, &hist_tokens);
+  if (e != DC_SUCCESS) return e;
+  const Board b{s0.bb[0], s0.bb[1], s0.bb[2], s0.bb[3]};
+  const char* d_names = c->hash_text.p;
+  HIP_TRY(c->timed("state_hash", n_games, [&] {
+    return dc::launch_state_hash_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, d_names, hist_len, hist_tokens,
+                                     d_names, c->hash_off.p, d_hashes);
+  }));
+  return sync_ctx(c);
+}
+
+}  // namespace
+
+extern "C" {
+
+int dc_keccak256(const void* data, size_t len, uint8_t out[32]) {
+  if ((!data && len) || !out) return DC_EINVAL;
+  dc::Keccak256 k;
+  k.update(data, len);
+  k.final(out);
+  return DC_SUCCESS;
+}
+
+int dc_state_hash_device(dc_ctx* c, const dc_pos* start, const char* history, const char* names,
+                         const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
+                         uint8_t* d_hashes) {
+  ENTER(c);
+  return state_hash_impl(c, start, history, names, names_off, d_moves, n_games, n_plies, d_hashes);
+}
+
+int dc_state_hash(dc_ctx* c, const dc_pos* start, const char* history, const char* names, const uint32_t* names_off,
+                  const uint16_t* moves, uint32_t n_games, uint32_t n_plies, uint8_t* hashes) {
+  ENTER(c);
+  if ((n_games && n_plies && !moves) || (n_games && !hashes)) return DC_EINVAL;
+  const size_t nm = (size_t)n_games * n_plies;
+  HIP_TRY(c->moves.ensure(std::max<size_t>(nm, 1)));
+  HIP_TRY(c->hashes.ensure(std::max<size_t>((size_t)32 * n_games, 1)));
+  if (nm) HIP_TRY(hipMemcpyAsync(c->moves.p, moves, nm * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  int r = state_hash_impl(c, start, history, names, names_off, c->moves.p, n_games, n_plies, c->hashes.p);
+  if (r != DC_SUCCESS) return r;
+  if (n_games) HIP_TRY(hipMemcpyAsync(hashes, c->hashes.p, (size_t)32 * n_games, hipMemcpyDeviceToHost, c->stream));
   return sync_ctx(c);
 }
 

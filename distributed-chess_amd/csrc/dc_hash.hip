@@ -1,0 +1,325 @@
+// dc_hash.hip -- the consensus state hash of replayed games on gfx950.
+//
+//   k_state_hash_ref   one lane per game: replay (RULES_REF), serialise the
+//                      final GameState as serde_json, keccak256 it
+//
+// What a replica computes before voting is keccak256(serde_json(GameState))
+// (core/src/consensus/hotstuff.rs:153-166; the same hash over a block at
+// core/src/consensus/types.rs:45-55).  For a batch of games this kernel gives
+// every game's final-state hash: a replay that ends in the value a replica
+// compares, i.e. a resync engine.
+//
+// The final state of game g: the start (turn, board, history) with the game's
+// accepted moves applied (chess.rs:43-80) and each one's notation appended to
+// the history (chess.rs:127-184: "N. san", N = whitespace tokens so far + 1).
+// JSON layout (serde_json, struct fields in prost's proto order, game.proto:7-40):
+//   {"turn":T,"white_player":"W","black_player":"B","history":"H",
+//    "board":{"rows":[{"cells":[{"piece":null},{"piece":{"color":0,"kind":"R"}},...]},...]}}
+// Names and the start history arrive JSON-escaped from the host; the tokens
+// the kernel appends are plain ASCII.
+//
+// Per lane: pass 1 replays the game to learn the final turn (the first JSON
+// field); pass 2 replays it again and streams the JSON bytes into the sponge.
+// Bytes are produced into the lane's 136-byte block in LDS by a small piece
+// state machine (template strings, names, start history, per-move tokens,
+// board cells); every lane emits exactly one block per step, so the
+// permutations of a wave run together until its lanes' streams end.
+#include <hip/hip_runtime.h>
+
+#include "dc_common.h"
+#include "dc_hash.h"
+#include "dc_keccak.h"
+
+namespace dc {
+
+// ----------------------------------------------------------- JSON templates
+// All fixed strings in one blob; a piece is (offset, length) in it.
+struct JsonTpl {
+  char s[640];
+  uint16_t off[24], len[24];
+};
+enum : int {
+  T_TURN = 0,   // {"turn":
+  T_DIGITS,     // 01
+  T_WP,         // ,"white_player":"
+  T_BP,         // ","black_player":"
+  T_HIST,       // ","history":"
+  T_BOARD,      // ","board":{"rows":[
+  T_ROW,        // {"cells":[
+  T_ROW_END,    // ]},   (the last row drops the comma)
+  T_END,        // ]}}
+  T_NULL,       // {"piece":null},   (the last cell of a row drops the comma)
+  T_CELL0,      // {"piece":{"color":0,"kind":"P"}},  ... 12 cells: colour-major P N B R Q K
+  T_COUNT = T_CELL0 + 12
+};
+
+constexpr JsonTpl make_json_tpl() {
+  JsonTpl t{};
+  const char* strs[T_COUNT] = {"{\"turn\":", "01", ",\"white_player\":\"", "\",\"black_player\":\"",
+                               "\",\"history\":\"", "\",\"board\":{\"rows\":[", "{\"cells\":[", "]},", "]}}",
+                               "{\"piece\":null},", nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int p = 0;
+  for (int i = 0; i < T_COUNT; ++i) {
+    t.off[i] = (uint16_t)p;
+    if (strs[i]) {
+      for (const char* c = strs[i]; *c; ++c) t.s[p++] = *c;
+    } else {  // {"piece":{"color":C,"kind":"K"}},
+      const int k = i - T_CELL0;
+      const char kinds[6] = {'P', 'N', 'B', 'R', 'Q', 'K'};
+      const char* a = "{\"piece\":{\"color\":";
+      for (const char* c = a; *c; ++c) t.s[p++] = *c;
+      t.s[p++] = (char)('0' + k / 6);
+      const char* b = ",\"kind\":\"";
+      for (const char* c = b; *c; ++c) t.s[p++] = *c;
+      t.s[p++] = kinds[k % 6];
+      t.s[p++] = '"';
+      t.s[p++] = '}';
+      t.s[p++] = '}';
+      t.s[p++] = ',';
+    }
+    t.len[i] = (uint16_t)(p - t.off[i]);
+  }
+  return t;
+}
+__constant__ JsonTpl g_json_tpl = make_json_tpl();
+
+// kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
+__device__ __forceinline__ u32 kind_index(u32 code) {
+  return code == KC_P ? 0 : code == KC_N ? 1 : code == KC_B ? 2 : code == KC_R ? 3 : code == KC_Q ? 4
+       : code == KC_K ? 5 : 6;
+}
+
+constexpr u32 kHashThreads = 256;
+constexpr u32 kTokBytes = 16;
+
+// Stages of a lane's JSON stream (in order).
+enum : u32 {
+  S_TURN, S_DIGIT, S_WP, S_WNAME, S_BP, S_BNAME, S_HIST, S_HSTART, S_TOKENS, S_BOARD, S_ROW, S_CELL, S_ROW_END,
+  S_END, S_DONE
+};
+
+__global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u32 stm0, const uint16_t* __restrict__ moves,
+                                                                  u32 n_games, u32 n_plies,
+                                                                  const char* __restrict__ hist, u32 hist_len,
+                                                                  u32 hist_tokens, const char* __restrict__ names,
+                                                                  const u32* __restrict__ names_off,
+                                                                  uint8_t* __restrict__ out) {
+  __shared__ char tpl[sizeof(g_json_tpl.s)];
+  __shared__ __attribute__((aligned(8))) uint8_t blk[kHashThreads][kKeccakRate];
+  __shared__ char tok[kHashThreads][kTokBytes];
+  const u32 tid = threadIdx.x;
+  for (u32 i = tid; i < sizeof(g_json_tpl.s); i += kHashThreads) tpl[i] = g_json_tpl.s[i];
+  __syncthreads();
+  const u32 g = blockIdx.x * kHashThreads + tid;
+  const bool active = g < n_games;
+  // ---- pass 1: the final turn
+  u32 stm = stm0;
+  if (active) {
+    Board b = start;
+    for (u32 p = 0; p < n_plies; ++p) {
+      const u32 m = moves[(size_t)p * n_games + g];
+      if (m != 0xFFFFu && ref_verdict(b, stm, m) == V_OK) {
+        ref_make(b, (int)(m & 63), (int)((m >> 6) & 63));
+        stm ^= 1;
+      }
+    }
+  }
+  // ---- pass 2: stream the JSON into the sponge
+  Board b = start;
+  u32 cur = stm0, ply = 0, ntok = hist_tokens;
+  u32 stage = active ? S_TURN : S_DONE;
+  bool glob = false;  // current piece is in global memory (names, start history)
+  u32 pos = g_json_tpl.off[T_TURN], rem = g_json_tpl.len[T_TURN];
+  u32 row = 0, col = 0;
+  const char* gsrc = nullptr;
+  u32 wn0 = 0, wn1 = 0, bn1 = 0;
+  if (active) {
+    wn0 = names_off[2 * g];
+    wn1 = names_off[2 * g + 1];
+    bn1 = names_off[2 * g + 2];
+  }
+  // Next non-empty piece after the current one ends.
+  auto advance = [&]() {
+    for (;;) {
+      glob = false;
+      switch (stage) {
+        case S_TURN:
+          stage = S_DIGIT;
+          pos = g_json_tpl.off[T_DIGITS] + stm;
+          rem = 1;
+          return;
+        case S_DIGIT:
+          stage = S_WP;
+          pos = g_json_tpl.off[T_WP];
+          rem = g_json_tpl.len[T_WP];
+          return;
+        case S_WP:
+          stage = S_WNAME;
+          glob = true;
+          gsrc = names;
+          pos = wn0;
+          rem = wn1 - wn0;
+          break;
+        case S_WNAME:
+          stage = S_BP;
+          pos = g_json_tpl.off[T_BP];
+          rem = g_json_tpl.len[T_BP];
+          return;
+        case S_BP:
+          stage = S_BNAME;
+          glob = true;
+          gsrc = names;
+          pos = wn1;
+          rem = bn1 - wn1;
+          break;
+        case S_BNAME:
+          stage = S_HIST;
+          pos = g_json_tpl.off[T_HIST];
+          rem = g_json_tpl.len[T_HIST];
+          return;
+        case S_HIST:
+          stage = S_HSTART;
+          glob = true;
+          gsrc = hist;
+          pos = 0;
+          rem = hist_len;
+          break;
+        case S_HSTART:
+          stage = S_TOKENS;
+          [[fallthrough]];
+        case S_TOKENS: {
+          // next accepted move: apply it and write its token "[ ]N. san"
+          bool found = false;
+          while (ply < n_plies && !found) {
+            const u32 m = moves[(size_t)ply * n_games + g];
+            ++ply;
+            if (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK) continue;
+            const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
+            const u32 ki = kind_index(nibble(b, f) >> 1);
+            const bool cap = (occupied(b) >> t) & 1;
+            char* w = tok[tid];
+            u32 n = 0;
+            if (ntok) w[n++] = ' ';
+            char dg[10];
+            u32 nd = 0, v = ntok + 1;
+            do {
+              dg[nd++] = (char)('0' + v % 10);
+              v /= 10;
+            } while (v);
+            while (nd) w[n++] = dg[--nd];
+            w[n++] = '.';
+            w[n++] = ' ';
+            if (ki != 0) w[n++] = "PNBRQK"[ki];
+            if (cap) {
+              if (ki == 0) w[n++] = (char)('a' + (f & 7));
+              w[n++] = 'x';
+            }
+            w[n++] = (char)('a' + (t & 7));
+            w[n++] = (char)('1' + (t >> 3));
+            ref_make(b, f, t);
+            cur ^= 1;
+            ntok += 2;
+            pos = (u32)(w - &tok[0][0]) + 0x10000u;  // tag: token buffer
+            rem = n;
+            found = true;
+          }
+          if (found) return;
+          stage = S_BOARD;
+          pos = g_json_tpl.off[T_BOARD];
+          rem = g_json_tpl.len[T_BOARD];
+          return;
+        }
+        case S_BOARD:
+        case S_ROW_END:
+          if (stage == S_ROW_END && row == 7) {
+            stage = S_END;
+            pos = g_json_tpl.off[T_END];
+            rem = g_json_tpl.len[T_END];
+            return;
+          }
+          if (stage == S_ROW_END) ++row;
+          stage = S_ROW;
+          col = 0;
+          pos = g_json_tpl.off[T_ROW];
+          rem = g_json_tpl.len[T_ROW];
+          return;
+        case S_ROW:
+        case S_CELL: {
+          if (stage == S_CELL && col == 7) {
+            stage = S_ROW_END;
+            pos = g_json_tpl.off[T_ROW_END];
+            rem = g_json_tpl.len[T_ROW_END] - (row == 7 ? 1u : 0u);
+            return;
+          }
+          if (stage == S_CELL) ++col;
+          stage = S_CELL;
+          const int sq = (int)(8 * row + col);
+          const u32 nib = nibble(b, sq);
+          const u32 ki = kind_index(nib >> 1);
+          const u32 ti = (nib >> 1) == 0 ? (u32)T_NULL : (u32)T_CELL0 + 6 * (nib & 1) + (ki < 6 ? ki : 0);
+          pos = g_json_tpl.off[ti];
+          rem = g_json_tpl.len[ti] - (col == 7 ? 1u : 0u);
+          return;
+        }
+        case S_END:
+        default:
+          stage = S_DONE;
+          rem = 0;
+          return;
+      }
+      if (rem) return;  // a global piece may be empty: try the next one
+    }
+  };
+  uint64_t a[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a[i] = 0;
+  bool padded = false, finished = !active;
+  uint8_t* my = blk[tid];
+  for (;;) {
+    const bool live = !finished;
+    if (__ballot(live) == 0) break;
+    if (live) {
+      for (u32 k = 0; k < kKeccakRate; ++k) {
+        u32 byte = 0;
+        if (stage != S_DONE) {
+          if (glob) byte = (uint8_t)gsrc[pos];
+          else if (pos & 0x10000u) byte = (uint8_t)(&tok[0][0])[pos & 0xFFFFu];
+          else byte = (uint8_t)tpl[pos];
+          ++pos;
+          if (--rem == 0) advance();
+        } else if (!padded) {
+          byte = 0x01;  // Keccak padding
+          padded = true;
+        }
+        my[k] = (uint8_t)byte;
+      }
+      if (padded) {
+        my[kKeccakRate - 1] |= 0x80;
+        finished = true;
+      }
+      const uint64_t* w = reinterpret_cast<const uint64_t*>(my);
+#pragma unroll
+      for (int i = 0; i < kKeccakRate / 8; ++i) a[i] ^= w[i];
+      keccak_f1600(a);
+    }
+  }
+  if (active) {
+    uint64_t* o = reinterpret_cast<uint64_t*>(out + (size_t)32 * g);
+    o[0] = a[0];
+    o[1] = a[1];
+    o[2] = a[2];
+    o[3] = a[3];
+  }
+}
+
+hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
+                                 u32 n_plies, const char* hist, u32 hist_len, u32 hist_tokens, const char* names,
+                                 const u32* names_off, uint8_t* out) {
+  if (n_games == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_state_hash_ref, dim3(blocks_for(n_games, kHashThreads)), dim3(kHashThreads), 0, st, start, stm0,
+                     moves, n_games, n_plies, hist, hist_len, hist_tokens, names, names_off, out);
+  return hipGetLastError();
+}
+
+}  // namespace dc

@@ -90,6 +90,10 @@ def lib():
                                      _vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
         "dc_multi_perft": (C.c_int, [_vp, C.c_int, C.c_uint32, _vp, C.c_uint32, _vp, _vp, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint64)]),
+        "dc_keccak256": (C.c_int, [_vp, C.c_size_t, _vp]),
+        "dc_state_hash": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
+        "dc_state_hash_device": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32,
+                                           _vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -117,6 +121,60 @@ def _ptr(a):
 
 def verdict_message(v):
     return lib().dc_verdict_message(v).decode()
+
+
+def keccak256(data):
+    """alloy_primitives::keccak256 of a byte string (host side of libdchess)."""
+    data = bytes(data)
+    buf = C.create_string_buffer(data, len(data)) if data else None
+    out = C.create_string_buffer(32)
+    _check(lib().dc_keccak256(C.cast(buf, _vp) if buf is not None else None, len(data), C.cast(out, _vp)),
+           "dc_keccak256")
+    return out.raw
+
+
+def pack_names(pairs):
+    """[(white, black), ...] -> (utf-8 blob, uint32 offsets[2n+1]) for dc_state_hash."""
+    blob, off = bytearray(), [0]
+    for w, b in pairs:
+        for name in (w, b):
+            blob += name.encode()
+            off.append(len(blob))
+    return bytes(blob), np.array(off, np.uint32)
+
+
+def _json_str(text):
+    """serde_json string literal (escape table of serde_json 1.0 ser.rs)."""
+    out = ['"']
+    for ch in text:
+        o = ord(ch)
+        if ch == '"':
+            out.append('\\"')
+        elif ch == "\\":
+            out.append("\\\\")
+        elif o < 0x20:
+            out.append({8: "\\b", 9: "\\t", 10: "\\n", 12: "\\f", 13: "\\r"}.get(o, "\\u%04x" % o))
+        else:
+            out.append(ch)
+    out.append('"')
+    return "".join(out)
+
+
+def game_state_json(turn, white, black, history, board):
+    """serde_json::to_string(&GameState) (core/proto/game.proto:7-40 via prost +
+    the serde derives of core/build.rs:2-32): fields in proto order, Option::None
+    as null, the i32 enum fields as numbers.  board[x][y] is None or a Piece."""
+    rows = []
+    for x in range(8):
+        cells = []
+        for y in range(8):
+            pc = board[x][y]
+            cells.append('{"piece":null}' if pc is None else
+                         '{"piece":{"color":%d,"kind":%s}}' % (pc.color, _json_str(pc.kind)))
+        rows.append('{"cells":[' + ",".join(cells) + "]}")
+    hist = "null" if history is None else _json_str(history)
+    return ('{"turn":%d,"white_player":%s,"black_player":%s,"history":%s,"board":{"rows":[%s]}}'
+            % (turn, _json_str(white), _json_str(black), hist, ",".join(rows)))
 
 
 # ---------------------------------------------------------------- positions
@@ -261,6 +319,24 @@ class Engine:
                                       C.byref(st)), "dc_replay_device")
         return {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
 
+    def state_hash(self, moves, names, start=None, history=""):
+        """keccak256(serde_json(final GameState)) of every game of a replay batch
+        (dc_state_hash).  moves: uint16 [n_plies, n_games]; names: [(white, black)]
+        per game.  Returns uint8 [n_games, 32]."""
+        moves = np.ascontiguousarray(moves, np.uint16)
+        n_plies, n_games = moves.shape
+        blob, off = pack_names(names)
+        assert len(off) == 2 * n_games + 1
+        out = np.zeros((n_games, 32), np.uint8)
+        sp = np.array([start], POS_DTYPE) if start is not None else None
+        _check(lib().dc_state_hash(self.ctx, _ptr(sp) if sp is not None else None, history.encode(), blob,
+                                   _ptr(off), _ptr(moves), n_games, n_plies, _ptr(out)), "dc_state_hash")
+        return out
+
+    def state_hash_device(self, d_moves, n_games, n_plies, names_blob, names_off, d_hashes, history=""):
+        _check(lib().dc_state_hash_device(self.ctx, None, history.encode(), names_blob, _ptr(names_off), d_moves.ptr,
+                                          n_games, n_plies, d_hashes.ptr), "dc_state_hash_device")
+
     def gen_games(self, seed, first_game, n_games, n_plies, noise_per_256=32, rules=RULES_REF):
         out = np.zeros((n_plies, n_games), np.uint16)
         _check(lib().dc_gen_games(self.ctx, rules, seed, first_game, n_games, n_plies, noise_per_256, _ptr(out)),
@@ -366,6 +442,15 @@ class GameState:
                     k = KINDS.index(p.kind) if p.kind in KINDS[:6] else 6
                     cells[8 * x + y] = p.color * 8 + k
         return pos_from_cells(cells, self.turn)
+
+    def to_json(self):
+        """serde_json::to_string(&GameState)."""
+        return game_state_json(self.turn, self.white_player, self.black_player, self.history, self.board)
+
+    def state_hash(self):
+        """calculate_game_state_hash (core/src/consensus/hotstuff.rs:153-166): keccak256 of
+        the JSON, as alloy's B256 Display string."""
+        return "0x" + keccak256(self.to_json().encode()).hex()
 
     def validate_move(self, frm, to):  # chess.rs:82-98
         v = self.engine.validate_batch(np.array([self._pos()], POS_DTYPE),

@@ -180,6 +180,34 @@ int dc_gen_games(dc_ctx* ctx, uint32_t rules, uint64_t seed, uint64_t first_game
 int dc_gen_games_device(dc_ctx* ctx, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games,
                         uint32_t n_plies, uint32_t noise_per_256, uint16_t* d_out);
 
+/* ------------------------------------------------------------- state hash
+ * The hash a replica compares before voting: keccak256(serde_json(GameState))
+ * (core/src/consensus/hotstuff.rs:153-166 calculate_game_state_hash; the same
+ * keccak-of-JSON as BlockBuilder::build, core/src/consensus/types.rs:45-55).
+ *
+ * dc_keccak256: alloy-primitives keccak256 (Keccak-256, padding 0x01..0x80)
+ * of one byte string, on the host -- the single-state path of the host
+ * mirrors.
+ *
+ * dc_state_hash: for every game of a replay batch, the hash of its FINAL
+ * GameState, on the GPU: start (dc_pos; NULL = startpos; turn = start.stm)
+ * plus the game's accepted moves (RULES_REF, chess.rs:43-80), each one's
+ * notation appended to `history` (chess.rs:127-184; the start history is
+ * shared by all games, NUL-terminated UTF-8, "" for GameState::new).  Player
+ * names: UTF-8 bytes names[names_off[2g] .. names_off[2g+1]) (white) and
+ * [names_off[2g+1] .. names_off[2g+2]) (black); names_off has 2*n_games+1
+ * entries.  hashes[32 g .. 32 g + 32) = the 32 digest bytes (alloy B256;
+ * "0x" + hex of them is calculate_game_state_hash's String).  A start board
+ * holding pieces of unknown kind returns DC_EUNSUPPORTED (their proto kind
+ * string is not representable in a dc_pos). */
+int dc_keccak256(const void* data, size_t len, uint8_t out[32]);
+int dc_state_hash(dc_ctx* ctx, const dc_pos* start, const char* history, const char* names,
+                  const uint32_t* names_off, const uint16_t* moves, uint32_t n_games, uint32_t n_plies,
+                  uint8_t* hashes);
+int dc_state_hash_device(dc_ctx* ctx, const dc_pos* start, const char* history, const char* names,
+                         const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
+                         uint8_t* d_hashes);
+
 /* -------------------------------------------------------------------- perft
  * perft(pos, depth) = number of leaf nodes of the move tree (under
  * REF the tree is every (from,to) pair validate_move accepts).  divide[i] is the

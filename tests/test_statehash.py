@@ -1,0 +1,163 @@
+"""State hash: keccak256(serde_json(GameState)),
+core/src/consensus/hotstuff.rs:153-166.
+
+CPU tests: the oracle (oracle/statehash.py) pinned against hashlib's SHA3-256
+(same Keccak-f[1600]) and keccak256("") (the padding); the host product
+(dc_keccak256, dchess.game_state_json) against the oracle.
+GPU tests (marked): dc_state_hash over replay batches against the oracle's
+move-by-move replay (refcpu verdicts, chess.rs history notation, JSON, keccak).
+The reference holds no test or fixture of this hash: parity of the JSON layout
+rests on prost/serde_json semantics restated in oracle/statehash.py (unpinned by
+the reference)."""
+import hashlib
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import dchess
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+import statehash as S  # noqa: E402
+
+
+# ------------------------------------------------------------------- CPU
+def test_oracle_keccak_pinned():
+    assert S.keccak256(b"").hex() == "c5d2460186f7233c927e7db2dcc703c0e500b653ca82273b7bfad8045d85a470"
+    rng = np.random.default_rng(1)
+    for n in (0, 1, 135, 136, 137, 271, 272, 1000, 3000):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert S.sha3_256(d) == hashlib.sha3_256(d).digest(), n
+
+
+def test_host_keccak_matches_oracle():
+    rng = np.random.default_rng(2)
+    for n in (0, 1, 7, 8, 135, 136, 137, 2500, 2999):
+        d = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert dchess.keccak256(d) == S.keccak256(d), n
+
+
+NAMES = ["Alice", "Bob", 'q"uo\\te', "tab\tnew\nline\x01\x1f", "Ümlaut ♞ 名前", ""]
+
+
+def _random_board(rng, n_pieces):
+    cells = np.full(64, -1, np.int8)
+    sq = rng.choice(64, n_pieces, replace=False)
+    cells[sq] = rng.integers(0, 2, n_pieces) * 8 + rng.integers(0, 6, n_pieces)
+    board = [[None] * 8 for _ in range(8)]
+    for s in range(64):
+        if cells[s] >= 0:
+            board[s // 8][s % 8] = dchess.Piece(cells[s] >> 3, S.KIND[cells[s] & 7])
+    return cells, board
+
+
+def test_game_state_json_matches_oracle():
+    rng = np.random.default_rng(3)
+    for i in range(20):
+        cells, board = _random_board(rng, int(rng.integers(0, 33)))
+        w, b = NAMES[i % len(NAMES)], NAMES[(i + 2) % len(NAMES)]
+        hist = None if i == 7 else ("" if i % 3 == 0 else "1. e4 3. Nf6 5. exd5")
+        turn = i & 1
+        assert dchess.game_state_json(turn, w, b, hist, board) == S.game_state_json(turn, w, b, hist, cells)
+
+
+def test_unknown_kind_string_serialised():
+    board = [[None] * 8 for _ in range(8)]
+    board[3][4] = dchess.Piece(1, "Dragon")
+    cells = np.full(64, -1, np.int8)
+    cells[28] = 8 + 6
+    assert dchess.game_state_json(0, "a", "b", "", board) == S.game_state_json(0, "a", "b", "", cells,
+                                                                               kinds={28: "Dragon"})
+
+
+# ------------------------------------------------------------------- GPU
+def _oracle_hashes(start, history, names, mv):
+    """Move-by-move: refcpu verdicts (chess.rs:82-125), apply (chess.rs:72-77),
+    update_history (chess.rs:127-184), serde_json, keccak256."""
+    import oracle_lib as O
+    n_plies, n_games = mv.shape
+    out = np.zeros((n_games, 32), np.uint8)
+    for g in range(n_games):
+        cells, stm, hist = start.cells.copy(), start.stm, history
+        for p in range(n_plies):
+            m = int(mv[p, g])
+            if m == O.SENTINEL or m & 0x8000:
+                continue
+            f, t = m & 63, (m >> 6) & 63
+            if O.ref_validate(cells, stm, f >> 3, f & 7, t >> 3, t & 7) != O.OK:
+                continue
+            hist = S.append_history(hist, S.notation(S.KIND[cells[f] & 7], cells[t] >= 0, f, t))
+            cells[t], cells[f] = cells[f], -1
+            stm ^= 1
+        w, b = names[g]
+        out[g] = np.frombuffer(S.keccak256(S.game_state_json(stm, w, b, hist, cells).encode()), np.uint8)
+    return out
+
+
+def _games(seed, n_games, n_plies, start):
+    import oracle_lib as O
+    rng = np.random.default_rng(seed)
+    mv = np.full((n_plies, n_games), O.SENTINEL, np.uint16)
+    for g in range(n_games):
+        p = start.copy()
+        for ply in range(n_plies if rng.random() < 0.85 else int(rng.integers(0, n_plies))):
+            legal = O.fast_gen_moves(p)
+            r = rng.random()
+            m = int(rng.choice(legal)) if (r < 0.75 and len(legal)) else (
+                int(rng.integers(0, 4096)) if r < 0.97 else 0x8000 | int(rng.integers(0, 0x7FFF)))
+            mv[ply, g] = m
+            if not m & 0x8000 and O.fast_validate(p, m) == O.OK:
+                p = O.fast_make(p, m)
+    return mv
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["startpos", "midgame_black_history"])
+def test_state_hash_batch_vs_oracle(engine, case):
+    import oracle_lib as O
+    if case == "startpos":
+        start, history, dstart = O.Pos(), "", None
+    else:
+        mv0 = O.fast_gen_games(77, 0, 1, 30, noise_per_256=0)
+        start = O.Pos()
+        for p in range(30):
+            start = O.fast_make(start, int(mv0[p, 0]))
+        start.castle, start.ep = 0, -1
+        start.stm = 1
+        history = "1. e4 3. e5\tnote  5. Nf3"
+        dstart = dchess.pos_from_cells(start.cells, start.stm)
+    n_games = 70 if case == "startpos" else 33
+    mv = _games(11, n_games, 41, start)
+    names = [(NAMES[g % len(NAMES)] + str(g), NAMES[(g * 5 + 1) % len(NAMES)]) for g in range(n_games)]
+    got = engine.state_hash(mv, names, start=dstart, history=history)
+    want = _oracle_hashes(start, history, names, mv)
+    assert (got == want).all()
+
+
+@pytest.mark.gpu
+def test_state_hash_matches_gamestate_mirror(engine):
+    """One game through the Python GameState mirror (dc_apply_batch per move,
+    host JSON + dc_keccak256) and through the batched kernel."""
+    import oracle_lib as O
+    gs = dchess.GameState("Alice", "Bob", engine)
+    mv = O.fast_gen_games(5, 0, 1, 24, noise_per_256=0)
+    for p in range(24):
+        m = int(mv[p, 0])
+        f, t = m & 63, (m >> 6) & 63
+        gs.apply_move(dchess.Position(f >> 3, f & 7), dchess.Position(t >> 3, t & 7))
+    got = engine.state_hash(mv, [("Alice", "Bob")])
+    assert "0x" + bytes(got[0]).hex() == gs.state_hash()
+
+
+@pytest.mark.gpu
+def test_state_hash_edge_cases(engine):
+    # no plies: the start state's hash; unknown-kind start rejected
+    got = engine.state_hash(np.zeros((0, 3), np.uint16), [("w", "b")] * 3)
+    import oracle_lib as O
+    want = S.keccak256(S.game_state_json(0, "w", "b", "", O.startpos_cells()).encode())
+    assert all(bytes(r) == want for r in got)
+    cells = np.full(64, -1, np.int8)
+    cells[0], cells[63] = 5, 8 + 6  # white king, black unknown kind
+    with pytest.raises(dchess.DChessError):
+        engine.state_hash(np.zeros((2, 1), np.uint16), [("w", "b")], start=dchess.pos_from_cells(cells, 0))
