@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--profile-only", action="store_true", help="run the steps, print nothing (rocprof)")
     ap.add_argument("--no-perft", action="store_true", help="with --profile-only: replay leg only (PMC passes)")
+    ap.add_argument("--hash-games", type=int, default=1_000_000, help="state-hash leg: games per rank (0: off)")
+    ap.add_argument("--hash-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -254,6 +256,39 @@ def roofline(ks, depth, world):
     return roof
 
 
+def state_hash_leg(eng, d, args):
+    """keccak256(serde_json(final GameState)) of every game of a seeded replay
+    batch (dc_state_hash_device): the hash a replica compares before voting
+    (core/src/consensus/hotstuff.rs:153-166), for a whole batch at once."""
+    n, plies = args.hash_games, args.plies
+    d_moves = eng.alloc(n * plies * 2)
+    d_h = eng.alloc(n * 32)
+    eng.gen_games_device(d_moves, 0x5EED20241022, d.rank * n, n, plies, 32)
+    blob, off = dchess.pack_names([(f"white{d.rank * n + g}", f"black{d.rank * n + g}") for g in range(n)])
+    eng.state_hash_device(d_moves, n, plies, blob, off, d_h)
+    d.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.hash_steps):
+        eng.state_hash_device(d_moves, n, plies, blob, off, d_h)
+    d.sync()
+    dt = d.max(time.perf_counter() - t0)
+    eng.reset_stats()
+    eng.set_profiling(True)
+    eng.state_hash_device(d_moves, n, plies, blob, off, d_h)
+    eng.set_profiling(False)
+    k = eng.kernel_stats("state_hash")
+    h0 = d_h.download(np.uint8, 32)
+    for b in (d_moves, d_h):
+        b.free()
+    total = n * d.world * args.hash_steps
+    return {"value": total / dt, "unit": "game state hashes/s", "scaling": "weak",
+            "workload": f"{n} seeded games x {plies} ply slots per rank: replay + serde_json(GameState) + keccak256 "
+                        "per game (names white<g>/black<g>, start history \"\")",
+            "ms_per_step": 1e3 * dt / args.hash_steps, "kernel_avg_ms": k["total_ms"] / max(k["launches"], 1),
+            "note": "includes the host-side JSON escaping + H2D of the names blob per call",
+            "first_hash": "0x" + bytes(h0).hex()}
+
+
 def main():
     args = parse()
     d = Dist(args.gpus)
@@ -310,6 +345,11 @@ def main():
         for b in (d_moves, d_bm, d_dg):
             b.free()
 
+    # ------------------------------------------- state hash
+    shash = None
+    if args.hash_games > 0 and not args.profile_only:
+        shash = state_hash_leg(eng, d, args)
+
     if d.rank != 0 or args.profile_only:
         return
     line = {
@@ -327,6 +367,8 @@ def main():
     }
     if p6 is not None:
         line["perft6"] = p6
+    if shash is not None:
+        line["state_hash"] = shash
     if replay is not None:
         line["replay"] = replay
     if not args.no_cpu and d.world == 1:
