@@ -126,175 +126,146 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
     }
   }
   // ---- pass 2: stream the JSON into the sponge
+  // The stream is a sequence of pieces (src, rem): template strings and tokens
+  // in LDS, names and the start history in global memory, all read through
+  // generic (flat) pointers so the byte copy has one code path.  A piece is
+  // chosen once (the divergent part) and then copied in runs.
   Board b = start;
   u32 cur = stm0, ply = 0, ntok = hist_tokens;
   u32 stage = active ? S_TURN : S_DONE;
-  bool glob = false;  // current piece is in global memory (names, start history)
-  u32 pos = g_json_tpl.off[T_TURN], rem = g_json_tpl.len[T_TURN];
+  const char* src = tpl + g_json_tpl.off[T_TURN];
+  u32 rem = active ? g_json_tpl.len[T_TURN] : 0u;
   u32 row = 0, col = 0;
-  const char* gsrc = nullptr;
   u32 wn0 = 0, wn1 = 0, bn1 = 0;
   if (active) {
     wn0 = names_off[2 * g];
     wn1 = names_off[2 * g + 1];
     bn1 = names_off[2 * g + 2];
   }
-  // Next non-empty piece after the current one ends.
-  auto advance = [&]() {
+  char* mytok = tok[tid];
+  auto tpl_piece = [&](int i, u32 drop) {
+    src = tpl + g_json_tpl.off[i];
+    rem = g_json_tpl.len[i] - drop;
+  };
+  // The piece after the current one (rem == 0: the stream has ended).
+  auto next_piece = [&]() {
     for (;;) {
-      glob = false;
       switch (stage) {
         case S_TURN:
           stage = S_DIGIT;
-          pos = g_json_tpl.off[T_DIGITS] + stm;
+          src = tpl + g_json_tpl.off[T_DIGITS] + stm;
           rem = 1;
-          return;
-        case S_DIGIT:
-          stage = S_WP;
-          pos = g_json_tpl.off[T_WP];
-          rem = g_json_tpl.len[T_WP];
-          return;
-        case S_WP:
-          stage = S_WNAME;
-          glob = true;
-          gsrc = names;
-          pos = wn0;
-          rem = wn1 - wn0;
           break;
-        case S_WNAME:
-          stage = S_BP;
-          pos = g_json_tpl.off[T_BP];
-          rem = g_json_tpl.len[T_BP];
-          return;
-        case S_BP:
-          stage = S_BNAME;
-          glob = true;
-          gsrc = names;
-          pos = wn1;
-          rem = bn1 - wn1;
-          break;
-        case S_BNAME:
-          stage = S_HIST;
-          pos = g_json_tpl.off[T_HIST];
-          rem = g_json_tpl.len[T_HIST];
-          return;
-        case S_HIST:
-          stage = S_HSTART;
-          glob = true;
-          gsrc = hist;
-          pos = 0;
-          rem = hist_len;
-          break;
+        case S_DIGIT: stage = S_WP; tpl_piece(T_WP, 0); break;
+        case S_WP: stage = S_WNAME; src = names + wn0; rem = wn1 - wn0; break;
+        case S_WNAME: stage = S_BP; tpl_piece(T_BP, 0); break;
+        case S_BP: stage = S_BNAME; src = names + wn1; rem = bn1 - wn1; break;
+        case S_BNAME: stage = S_HIST; tpl_piece(T_HIST, 0); break;
+        case S_HIST: stage = S_HSTART; src = hist; rem = hist_len; break;
         case S_HSTART:
-          stage = S_TOKENS;
-          [[fallthrough]];
         case S_TOKENS: {
+          stage = S_TOKENS;
           // next accepted move: apply it and write its token "[ ]N. san"
-          bool found = false;
-          while (ply < n_plies && !found) {
+          rem = 0;
+          while (ply < n_plies && rem == 0) {
             const u32 m = moves[(size_t)ply * n_games + g];
             ++ply;
             if (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK) continue;
             const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
             const u32 ki = kind_index(nibble(b, f) >> 1);
             const bool cap = (occupied(b) >> t) & 1;
-            char* w = tok[tid];
             u32 n = 0;
-            if (ntok) w[n++] = ' ';
+            if (ntok) mytok[n++] = ' ';
             char dg[10];
             u32 nd = 0, v = ntok + 1;
             do {
               dg[nd++] = (char)('0' + v % 10);
               v /= 10;
             } while (v);
-            while (nd) w[n++] = dg[--nd];
-            w[n++] = '.';
-            w[n++] = ' ';
-            if (ki != 0) w[n++] = "PNBRQK"[ki];
+            while (nd) mytok[n++] = dg[--nd];
+            mytok[n++] = '.';
+            mytok[n++] = ' ';
+            if (ki != 0) mytok[n++] = "PNBRQK"[ki];
             if (cap) {
-              if (ki == 0) w[n++] = (char)('a' + (f & 7));
-              w[n++] = 'x';
+              if (ki == 0) mytok[n++] = (char)('a' + (f & 7));
+              mytok[n++] = 'x';
             }
-            w[n++] = (char)('a' + (t & 7));
-            w[n++] = (char)('1' + (t >> 3));
+            mytok[n++] = (char)('a' + (t & 7));
+            mytok[n++] = (char)('1' + (t >> 3));
             ref_make(b, f, t);
             cur ^= 1;
             ntok += 2;
-            pos = (u32)(w - &tok[0][0]) + 0x10000u;  // tag: token buffer
+            src = mytok;
             rem = n;
-            found = true;
           }
-          if (found) return;
-          stage = S_BOARD;
-          pos = g_json_tpl.off[T_BOARD];
-          rem = g_json_tpl.len[T_BOARD];
-          return;
+          if (rem == 0) {
+            stage = S_BOARD;
+            tpl_piece(T_BOARD, 0);
+          }
+          break;
         }
         case S_BOARD:
-        case S_ROW_END:
-          if (stage == S_ROW_END && row == 7) {
-            stage = S_END;
-            pos = g_json_tpl.off[T_END];
-            rem = g_json_tpl.len[T_END];
-            return;
-          }
-          if (stage == S_ROW_END) ++row;
           stage = S_ROW;
-          col = 0;
-          pos = g_json_tpl.off[T_ROW];
-          rem = g_json_tpl.len[T_ROW];
-          return;
+          row = 0;
+          tpl_piece(T_ROW, 0);
+          break;
+        case S_ROW_END:
+          if (row == 7) {
+            stage = S_END;
+            tpl_piece(T_END, 0);
+            break;
+          }
+          ++row;
+          stage = S_ROW;
+          tpl_piece(T_ROW, 0);
+          break;
         case S_ROW:
         case S_CELL: {
           if (stage == S_CELL && col == 7) {
             stage = S_ROW_END;
-            pos = g_json_tpl.off[T_ROW_END];
-            rem = g_json_tpl.len[T_ROW_END] - (row == 7 ? 1u : 0u);
-            return;
+            tpl_piece(T_ROW_END, row == 7 ? 1u : 0u);
+            break;
           }
-          if (stage == S_CELL) ++col;
+          col = stage == S_ROW ? 0u : col + 1;
           stage = S_CELL;
-          const int sq = (int)(8 * row + col);
-          const u32 nib = nibble(b, sq);
+          const u32 nib = nibble(b, (int)(8 * row + col));
           const u32 ki = kind_index(nib >> 1);
-          const u32 ti = (nib >> 1) == 0 ? (u32)T_NULL : (u32)T_CELL0 + 6 * (nib & 1) + (ki < 6 ? ki : 0);
-          pos = g_json_tpl.off[ti];
-          rem = g_json_tpl.len[ti] - (col == 7 ? 1u : 0u);
-          return;
+          const int ti = (nib >> 1) == 0 ? (int)T_NULL : (int)T_CELL0 + 6 * (int)(nib & 1) + (ki < 6 ? (int)ki : 0);
+          tpl_piece(ti, col == 7 ? 1u : 0u);
+          break;
         }
-        case S_END:
-        default:
+        default:  // S_END
           stage = S_DONE;
           rem = 0;
           return;
       }
-      if (rem) return;  // a global piece may be empty: try the next one
+      if (rem) return;  // names and the start history may be empty
     }
   };
   uint64_t a[25];
 #pragma unroll
   for (int i = 0; i < 25; ++i) a[i] = 0;
-  bool padded = false, finished = !active;
+  bool finished = !active;
   uint8_t* my = blk[tid];
   for (;;) {
-    const bool live = !finished;
-    if (__ballot(live) == 0) break;
-    if (live) {
-      for (u32 k = 0; k < kKeccakRate; ++k) {
-        u32 byte = 0;
-        if (stage != S_DONE) {
-          if (glob) byte = (uint8_t)gsrc[pos];
-          else if (pos & 0x10000u) byte = (uint8_t)(&tok[0][0])[pos & 0xFFFFu];
-          else byte = (uint8_t)tpl[pos];
-          ++pos;
-          if (--rem == 0) advance();
-        } else if (!padded) {
-          byte = 0x01;  // Keccak padding
-          padded = true;
+    if (__ballot(!finished) == 0) break;
+    if (!finished) {
+      // fill this step's 136-byte block
+      u32 fill = 0;
+      while (fill < (u32)kKeccakRate && stage != S_DONE) {
+        if (rem == 0) {
+          next_piece();
+          continue;
         }
-        my[k] = (uint8_t)byte;
+        const u32 n = min(rem, (u32)kKeccakRate - fill);
+        for (u32 k = 0; k < n; ++k) my[fill + k] = (uint8_t)src[k];
+        src += n;
+        rem -= n;
+        fill += n;
       }
-      if (padded) {
+      if (fill < (u32)kKeccakRate) {  // the stream ended in this block: Keccak padding
+        my[fill] = 0x01;
+        for (u32 k = fill + 1; k < (u32)kKeccakRate; ++k) my[k] = 0;
         my[kKeccakRate - 1] |= 0x80;
         finished = true;
       }

@@ -90,10 +90,100 @@ DC_HD void keccak_round(uint64_t* a, uint64_t rc) {
   a[0] ^= rc;
 }
 
-DC_HD void keccak_f1600(uint64_t* a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950 form of the same round: 64-bit lanes as (lo, hi) halves so that
+// xor3 and chi's a ^ (~b & c) are one v_bitop3_b32 per half and a rotate is
+// two v_alignbit_b32 (the generic form compiled to 64-bit shift pairs).
+struct K64 {
+  uint32_t lo, hi;
+};
+template <unsigned IMM>
+__device__ __forceinline__ uint32_t kb3(uint32_t a, uint32_t b, uint32_t c) {
+  return (uint32_t)__builtin_amdgcn_bitop3_b32(a, b, c, IMM);
+}
+__device__ __forceinline__ uint32_t kal(uint32_t a, uint32_t b, uint32_t s) {
+  return (uint32_t)__builtin_amdgcn_alignbit(a, b, s);
+}
+__device__ __forceinline__ K64 kx3(K64 a, K64 b, K64 c) {  // a ^ b ^ c
+  return K64{kb3<0x96>(a.lo, b.lo, c.lo), kb3<0x96>(a.hi, b.hi, c.hi)};
+}
+__device__ __forceinline__ K64 kx2(K64 a, K64 b) { return K64{a.lo ^ b.lo, a.hi ^ b.hi}; }
+__device__ __forceinline__ K64 kchi(K64 a, K64 b, K64 c) {  // a ^ (~b & c)
+  return K64{kb3<0xD2>(a.lo, b.lo, c.lo), kb3<0xD2>(a.hi, b.hi, c.hi)};
+}
+template <int N>
+__device__ __forceinline__ K64 krot(K64 x) {
+  if constexpr (N == 0) return x;
+  else if constexpr (N == 32) return K64{x.hi, x.lo};
+  else if constexpr (N < 32)
+    return K64{kal(x.lo, x.hi, 32 - N), kal(x.hi, x.lo, 32 - N)};
+  else
+    return K64{kal(x.hi, x.lo, 64 - N), kal(x.lo, x.hi, 64 - N)};
+}
+
+__device__ __forceinline__ void keccak_f1600_dev(uint64_t* a64) {
   constexpr KeccakRC rc = keccak_rc();
+  K64 a[25];
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a[i] = K64{(uint32_t)a64[i], (uint32_t)(a64[i] >> 32)};
 #pragma unroll 1
+  for (int r = 0; r < 24; ++r) {
+    const K64 c0 = kx3(kx3(a[0], a[5], a[10]), a[15], a[20]);
+    const K64 c1 = kx3(kx3(a[1], a[6], a[11]), a[16], a[21]);
+    const K64 c2 = kx3(kx3(a[2], a[7], a[12]), a[17], a[22]);
+    const K64 c3 = kx3(kx3(a[3], a[8], a[13]), a[18], a[23]);
+    const K64 c4 = kx3(kx3(a[4], a[9], a[14]), a[19], a[24]);
+    const K64 d0 = kx2(c4, krot<1>(c1)), d1 = kx2(c0, krot<1>(c2)), d2 = kx2(c1, krot<1>(c3));
+    const K64 d3 = kx2(c2, krot<1>(c4)), d4 = kx2(c3, krot<1>(c0));
+    K64 b[25];
+    b[0] = kx2(a[0], d0);
+    b[10] = krot<1>(kx2(a[1], d1));
+    b[20] = krot<62>(kx2(a[2], d2));
+    b[5] = krot<28>(kx2(a[3], d3));
+    b[15] = krot<27>(kx2(a[4], d4));
+    b[16] = krot<36>(kx2(a[5], d0));
+    b[1] = krot<44>(kx2(a[6], d1));
+    b[11] = krot<6>(kx2(a[7], d2));
+    b[21] = krot<55>(kx2(a[8], d3));
+    b[6] = krot<20>(kx2(a[9], d4));
+    b[7] = krot<3>(kx2(a[10], d0));
+    b[17] = krot<10>(kx2(a[11], d1));
+    b[2] = krot<43>(kx2(a[12], d2));
+    b[12] = krot<25>(kx2(a[13], d3));
+    b[22] = krot<39>(kx2(a[14], d4));
+    b[23] = krot<41>(kx2(a[15], d0));
+    b[8] = krot<45>(kx2(a[16], d1));
+    b[18] = krot<15>(kx2(a[17], d2));
+    b[3] = krot<21>(kx2(a[18], d3));
+    b[13] = krot<8>(kx2(a[19], d4));
+    b[14] = krot<18>(kx2(a[20], d0));
+    b[24] = krot<2>(kx2(a[21], d1));
+    b[9] = krot<61>(kx2(a[22], d2));
+    b[19] = krot<56>(kx2(a[23], d3));
+    b[4] = krot<14>(kx2(a[24], d4));
+#pragma unroll
+    for (int y = 0; y < 25; y += 5) {
+      a[y] = kchi(b[y], b[y + 1], b[y + 2]);
+      a[y + 1] = kchi(b[y + 1], b[y + 2], b[y + 3]);
+      a[y + 2] = kchi(b[y + 2], b[y + 3], b[y + 4]);
+      a[y + 3] = kchi(b[y + 3], b[y + 4], b[y]);
+      a[y + 4] = kchi(b[y + 4], b[y], b[y + 1]);
+    }
+    a[0].lo ^= (uint32_t)rc.v[r];
+    a[0].hi ^= (uint32_t)(rc.v[r] >> 32);
+  }
+#pragma unroll
+  for (int i = 0; i < 25; ++i) a64[i] = ((uint64_t)a[i].hi << 32) | a[i].lo;
+}
+#endif
+
+DC_HD void keccak_f1600(uint64_t* a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  keccak_f1600_dev(a);
+#else
+  constexpr KeccakRC rc = keccak_rc();
   for (int r = 0; r < 24; ++r) keccak_round(a, rc.v[r]);
+#endif
 }
 
 constexpr int kKeccakRate = 136;  // bytes: 1600 - 2 x 256 bits of capacity
