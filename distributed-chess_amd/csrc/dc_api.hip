@@ -558,7 +558,14 @@ namespace {
 // other byte, UTF-8 included, verbatim.
 void json_escape(const char* s, size_t n, std::string& out) {
   static const char hex[] = "0123456789abcdef";
-  for (size_t i = 0; i < n; ++i) {
+  size_t clean = 0;  // fast path: a run of bytes that need no escape is appended whole
+  while (clean < n) {
+    const unsigned char ch = (unsigned char)s[clean];
+    if (ch < 0x20 || ch == '"' || ch == '\\') break;
+    ++clean;
+  }
+  out.append(s, clean);
+  for (size_t i = clean; i < n; ++i) {
     const unsigned char ch = (unsigned char)s[i];
     switch (ch) {
       case '"': out += "\\\""; break;
@@ -609,6 +616,7 @@ int stage_hash_text(dc_ctx* c, const char* history, const char* names, const uin
                     u32* hist_len, u32* hist_tokens) {
   const size_t hn = history ? std::strlen(history) : 0;
   std::string text;
+  text.reserve(hn + (size_t)names_off[(size_t)2 * n_games] + 64);
   json_escape(history ? history : "", hn, text);
   *hist_len = (u32)text.size();
   *hist_tokens = count_ws_tokens(history ? history : "", hn);
