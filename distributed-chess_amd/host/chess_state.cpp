@@ -23,6 +23,75 @@ std::optional<AppError> verdict_to_result(uint8_t v) {
 }
 }  // namespace
 
+namespace {
+// serde_json string literal (serde_json 1.0 ser.rs ESCAPE table).
+void json_str(const std::string& v, std::string& out) {
+  static const char hex[] = "0123456789abcdef";
+  out += '"';
+  for (unsigned char ch : v) {
+    switch (ch) {
+      case '"': out += "\\\""; break;
+      case '\\': out += "\\\\"; break;
+      case '\b': out += "\\b"; break;
+      case '\t': out += "\\t"; break;
+      case '\n': out += "\\n"; break;
+      case '\f': out += "\\f"; break;
+      case '\r': out += "\\r"; break;
+      default:
+        if (ch < 0x20) {
+          out += "\\u00";
+          out += hex[ch >> 4];
+          out += hex[ch & 15];
+        } else {
+          out += (char)ch;
+        }
+    }
+  }
+  out += '"';
+}
+}  // namespace
+
+std::string GameState::to_json() const {
+  std::string j = "{\"turn\":" + std::to_string(turn) + ",\"white_player\":";
+  json_str(white_player, j);
+  j += ",\"black_player\":";
+  json_str(black_player, j);
+  j += ",\"history\":";
+  if (history) json_str(*history, j);
+  else j += "null";
+  j += ",\"board\":{\"rows\":[";
+  for (int x = 0; x < 8; ++x) {
+    j += x ? ",{\"cells\":[" : "{\"cells\":[";
+    for (int y = 0; y < 8; ++y) {
+      if (y) j += ',';
+      const auto& p = board[x][y];
+      if (!p) {
+        j += "{\"piece\":null}";
+      } else {
+        j += "{\"piece\":{\"color\":" + std::to_string(p->color) + ",\"kind\":";
+        json_str(p->kind, j);
+        j += "}}";
+      }
+    }
+    j += "]}";
+  }
+  j += "]}}";
+  return j;
+}
+
+std::string GameState::state_hash() const {
+  const std::string j = to_json();
+  uint8_t h[32];
+  check(dc_keccak256(j.data(), j.size(), h), "dc_keccak256");
+  static const char hex[] = "0123456789abcdef";
+  std::string s = "0x";
+  for (uint8_t b : h) {
+    s += hex[b >> 4];
+    s += hex[b & 15];
+  }
+  return s;
+}
+
 Engine::Engine(int device) { check(dc_ctx_create(device, &ctx_), "dc_ctx_create"); }
 Engine::~Engine() {
   if (ctx_) dc_ctx_destroy(ctx_);

@@ -73,6 +73,13 @@ struct GameState {  // proto game.GameState, core/proto/game.proto:7-13
                                                             const std::vector<std::pair<Position, Position>>& moves);
 
   dc_pos to_pos() const;
+
+  // serde_json::to_string(&GameState) (fields in proto order, None -> null,
+  // prost i32 enums as numbers, serde_json string escapes) and
+  // calculate_game_state_hash (core/src/consensus/hotstuff.rs:153-166):
+  // "0x" + hex(keccak256(json)), keccak through dc_keccak256.
+  std::string to_json() const;
+  std::string state_hash() const;
 };
 
 }  // namespace dchess

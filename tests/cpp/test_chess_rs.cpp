@@ -78,7 +78,25 @@ static void test_errors_and_history(Engine& e) {
   CHECK(rej && rej->message == "It's not this piece's turn to move" && *g.history == "1. e4 3. e5 5. Bc4");
 }
 
-int main() {
+// --json: serde_json(GameState) + calculate_game_state_hash of a fixed state
+// (host only, no device), checked by tests/test_cpp_host.py against the oracle.
+static int print_json_case() {
+  GameState g = GameState::create("Al\"ice\\", "B\tob\x01");
+  g.history = std::string("1. e4 3. e5");
+  g.board[3][4] = g.board[1][4];
+  g.board[1][4].reset();
+  g.board[4][4] = g.board[6][4];
+  g.board[6][4].reset();
+  g.board[5][5] = dchess::Piece{1, "Dragon"};
+  std::printf("%s\n%s\n", g.to_json().c_str(), g.state_hash().c_str());
+  g.history.reset();
+  g.turn = 1;
+  std::printf("%s\n%s\n", g.to_json().c_str(), g.state_hash().c_str());
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc > 1 && std::strcmp(argv[1], "--json") == 0) return print_json_case();
   try {
     Engine e(0);
     test_initial_game_state();
