@@ -24,6 +24,7 @@
 #include "dc_keccak.h"
 #include "dc_kernels.h"
 #include "dc_perft.h"
+#include "dc_txsig_k.h"
 
 using dc::Board;
 using dc::DevPos;
@@ -120,8 +121,22 @@ struct dc_ctx {
   DBuf<u32> hash_off;
   DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
+  // transaction-signature check: staged strings / offsets / actions / turns,
+  // and the G table (built on first use)
+  DBuf<char> tx_text;
+  DBuf<u32> tx_off, tx_act;
+  DBuf<int8_t> tx_turn;
+  DBuf<uint8_t> tx_verdicts;
+  DBuf<dc::secp::Ge> gtab;
+  bool gtab_ready = false;
 
   ~dc_ctx() {
+    tx_text.release();
+    tx_off.release();
+    tx_act.release();
+    tx_turn.release();
+    tx_verdicts.release();
+    gtab.release();
     for (auto* b : {&nodes[0], &nodes[1], &top_nodes, &root}) b->release();
     for (auto* b : {&tags[0], &tags[1], &meta[0], &meta[1], &top_tags, &top_meta, &root_meta, &moves}) b->release();
     counts.release();
@@ -688,6 +703,66 @@ int dc_state_hash(dc_ctx* c, const dc_pos* start, const char* history, const cha
   int r = state_hash_impl(c, start, history, names, names_off, c->moves.p, n_games, n_plies, c->hashes.p);
   if (r != DC_SUCCESS) return r;
   if (n_games) HIP_TRY(hipMemcpyAsync(hashes, c->hashes.p, (size_t)32 * n_games, hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+// ------------------------------------------------ transaction signatures
+const char* dc_sig_verdict_message(uint8_t v) {
+  switch (v) {
+    case DC_SIG_OK: return "";
+    case DC_SIG_BAD_SIG_HEX: return "invalid signature hex";
+    case DC_SIG_BAD_SIG: return "invalid signature encoding";
+    case DC_SIG_BAD_PK_HEX: return "invalid public key hex";
+    case DC_SIG_BAD_PK: return "invalid public key";
+    case DC_SIG_INVALID: return "invalid signature";  // hotstuff.rs:204-206
+    case DC_SIG_WRONG_OWNER: return "invalud turn";    // hotstuff.rs:147 (sic)
+  }
+  return "unknown verdict";
+}
+
+static int ensure_gtab(dc_ctx* c) {
+  if (c->gtab_ready) return DC_SUCCESS;
+  HIP_TRY(c->gtab.ensure(dc::secp::kGTabEntries));
+  HIP_TRY(dc::launch_secp_gtab(c->stream, c->gtab.p));
+  c->gtab_ready = true;
+  return DC_SUCCESS;
+}
+
+int dc_verify_tx_batch_device(dc_ctx* c, const char* d_strings, const uint32_t* d_str_off, const uint32_t* d_actions,
+                              const int8_t* d_turns, uint32_t n, uint8_t* d_verdicts) {
+  ENTER(c);
+  if (n == 0) return DC_SUCCESS;
+  if (!d_strings || !d_str_off || !d_actions || !d_verdicts) return DC_EINVAL;
+  int e = ensure_gtab(c);
+  if (e != DC_SUCCESS) return e;
+  HIP_TRY(c->timed("verify_tx", n, [&] {
+    return dc::launch_verify_tx(c->stream, d_strings, d_str_off, d_actions, d_turns, n, c->gtab.p, d_verdicts);
+  }));
+  return sync_ctx(c);
+}
+
+int dc_verify_tx_batch(dc_ctx* c, const char* strings, const uint32_t* str_off, const uint32_t* actions,
+                       const int8_t* turns, uint32_t n, uint8_t* verdicts) {
+  ENTER(c);
+  if (n == 0) return DC_SUCCESS;
+  if (!strings || !str_off || !actions || !verdicts) return DC_EINVAL;
+  const size_t no = (size_t)4 * n + 1;
+  for (size_t i = 0; i + 1 < no; ++i)
+    if (str_off[i + 1] < str_off[i]) return DC_EINVAL;
+  const size_t nt = str_off[no - 1];
+  HIP_TRY(c->tx_text.ensure(std::max<size_t>(nt, 1)));
+  HIP_TRY(c->tx_off.ensure(no));
+  HIP_TRY(c->tx_act.ensure((size_t)4 * n));
+  HIP_TRY(c->tx_verdicts.ensure(n));
+  if (turns) HIP_TRY(c->tx_turn.ensure(n));
+  if (nt) HIP_TRY(hipMemcpyAsync(c->tx_text.p, strings, nt, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->tx_off.p, str_off, no * sizeof(u32), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->tx_act.p, actions, (size_t)4 * n * sizeof(u32), hipMemcpyHostToDevice, c->stream));
+  if (turns) HIP_TRY(hipMemcpyAsync(c->tx_turn.p, turns, n, hipMemcpyHostToDevice, c->stream));
+  const int r = dc_verify_tx_batch_device(c, c->tx_text.p, c->tx_off.p, c->tx_act.p, turns ? c->tx_turn.p : nullptr,
+                                          n, c->tx_verdicts.p);
+  if (r != DC_SUCCESS) return r;
+  HIP_TRY(hipMemcpyAsync(verdicts, c->tx_verdicts.p, n, hipMemcpyDeviceToHost, c->stream));
   return sync_ctx(c);
 }
 

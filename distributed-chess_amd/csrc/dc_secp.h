@@ -1,0 +1,701 @@
+// dc_secp.h -- secp256k1 field, scalar and point arithmetic for the batched
+// transaction-signature check (k_verify_tx, dc_txsig.hip).
+//
+// What it restates: libsecp256k1 0.7.1 (core/Cargo.lock), as called by
+// App::validate_signature (core/src/consensus/hotstuff.rs:168-208):
+//   field  F_p, p = 2^256 - 2^32 - 977       (2^256 = 2^32 + 977 mod p)
+//   scalar Z_n, n = 2^256 - C, C = 0x14551231950B75FC4402DA1732FC9BEBF
+//   curve  y^2 = x^3 + 7, generator G
+//
+// Representation for a 32-bit VALU: 8 little-endian u32 limbs, always
+// canonical (< p resp. < n) after every operation, so equality is limb
+// equality and parity is bit 0.  Products are operand-scanned with 64-bit
+// multiply-adds (v_mad_u64_u32: a*b + c + d never overflows 64 bits) and
+// folded with the special form of p (one 977-multiply pass plus a shifted
+// add) or of n (four passes of the 129-bit C).
+//
+// Every function is __host__ __device__: the same code runs in the gfx950
+// kernel and in a host unit-test binary (tests/cpp/test_secp.cpp) that checks
+// it against oracle/txsig.py on the CPU of this container.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#define SECP_HD __host__ __device__ __forceinline__
+
+namespace dc {
+namespace secp {
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+struct Fe {
+  u32 v[8];
+};
+struct Sc {
+  u32 v[8];
+};
+struct Ge {  // affine point (never the point at infinity)
+  Fe x, y;
+};
+struct Gej {  // Jacobian point: (X / Z^2, Y / Z^3), or infinity
+  Fe x, y, z;
+  u32 inf;
+};
+
+// ------------------------------------------------------------------ limbs
+SECP_HD void set_zero(u32 (&a)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = 0;
+}
+SECP_HD bool is_zero8(const u32 (&a)[8]) {
+  u32 o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o |= a[i];
+  return o == 0;
+}
+SECP_HD bool eq8(const u32 (&a)[8], const u32 (&b)[8]) {
+  u32 o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o |= a[i] ^ b[i];
+  return o == 0;
+}
+SECP_HD void sel8(u32 (&r)[8], bool c, const u32 (&a)[8], const u32 (&b)[8]) {  // r = c ? a : b
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = c ? a[i] : b[i];
+}
+// 32 big-endian bytes -> limbs (no reduction)
+SECP_HD void from_be32(u32 (&r)[8], const uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint8_t* q = b + 28 - 4 * i;
+    r[i] = ((u32)q[0] << 24) | ((u32)q[1] << 16) | ((u32)q[2] << 8) | (u32)q[3];
+  }
+}
+SECP_HD void to_be32(const u32 (&a)[8], uint8_t* b) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint8_t* q = b + 28 - 4 * i;
+    q[0] = (uint8_t)(a[i] >> 24);
+    q[1] = (uint8_t)(a[i] >> 16);
+    q[2] = (uint8_t)(a[i] >> 8);
+    q[3] = (uint8_t)a[i];
+  }
+}
+
+// ------------------------------------------------------------- field F_p
+constexpr u32 kP977 = 977u;
+
+// r = a + (2^32 + 977) mod 2^256; returns the carry out (1 iff a >= p).
+SECP_HD u32 add_k(u32 (&r)[8], const u32 (&a)[8]) {
+  u64 d = (u64)a[0] + kP977;
+  r[0] = (u32)d;
+  d = (d >> 32) + (u64)a[1] + 1u;
+  r[1] = (u32)d;
+  d >>= 32;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    d += a[i];
+    r[i] = (u32)d;
+    d >>= 32;
+  }
+  return (u32)d;
+}
+
+SECP_HD bool fe_lt_p(const u32 (&a)[8]) {
+  u32 t[8];
+  return add_k(t, a) == 0;
+}
+
+// a (< 2^256) -> a mod p (one conditional subtraction suffices: a < 2p)
+SECP_HD void fe_canon(Fe& r, const u32 (&a)[8]) {
+  u32 t[8];
+  const u32 ge = add_k(t, a);
+  sel8(r.v, ge != 0, t, a);
+}
+
+SECP_HD void fe_set_u32(Fe& r, u32 x) {
+  set_zero(r.v);
+  r.v[0] = x;
+}
+
+SECP_HD void fe_add(Fe& r, const Fe& a, const Fe& b) {
+  u32 s[8], t[8];
+  u64 c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (u64)a.v[i] + b.v[i];
+    s[i] = (u32)c;
+    c >>= 32;
+  }
+  // a + b < 2p: if it overflowed 2^256 or s >= p, the result is s + (2^256 - p)
+  const u32 d = add_k(t, s);
+  sel8(r.v, (c | d) != 0, t, s);
+}
+
+SECP_HD void fe_sub(Fe& r, const Fe& a, const Fe& b) {
+  u32 s[8];
+  u64 br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const u64 t = (u64)a.v[i] - b.v[i] - br;
+    s[i] = (u32)t;
+    br = (t >> 32) & 1u;
+  }
+  // borrow: add p, i.e. subtract 2^32 + 977 modulo 2^256
+  const u32 m = (u32)br;
+  u64 t = (u64)s[0] - (m * kP977);
+  r.v[0] = (u32)t;
+  u64 b2 = (t >> 32) & 1u;
+  t = (u64)s[1] - m - b2;
+  r.v[1] = (u32)t;
+  b2 = (t >> 32) & 1u;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    t = (u64)s[i] - b2;
+    r.v[i] = (u32)t;
+    b2 = (t >> 32) & 1u;
+  }
+}
+
+SECP_HD void fe_neg(Fe& r, const Fe& a) {
+  Fe z;
+  set_zero(z.v);
+  fe_sub(r, z, a);
+}
+
+// 512-bit product a * b (operand scanning; each step a*b + t + c < 2^64)
+SECP_HD void mul_wide(u32 (&t)[16], const u32 (&a)[8], const u32 (&b)[8]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const u64 x = (u64)a[i] * b[j] + t[i + j] + c;
+      t[i + j] = (u32)x;
+      c = x >> 32;
+    }
+    t[i + 8] = (u32)c;
+  }
+}
+
+// 512-bit square: cross products once, doubled, plus the diagonal
+SECP_HD void sqr_wide(u32 (&t)[16], const u32 (&a)[8]) {
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; ++j) {
+      const u64 x = (u64)a[i] * a[j] + t[i + j] + c;
+      t[i + j] = (u32)x;
+      c = x >> 32;
+    }
+    t[i + 8] = (u32)c;
+  }
+  // double the cross products
+  u32 hi = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const u32 x = t[i];
+    t[i] = (x << 1) | hi;
+    hi = x >> 31;
+  }
+  // add the squares a[i]^2 at limb 2i
+  u64 c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const u64 sq = (u64)a[i] * a[i];
+    c += (u64)t[2 * i] + (u32)sq;
+    t[2 * i] = (u32)c;
+    c >>= 32;
+    c += (u64)t[2 * i + 1] + (u32)(sq >> 32);
+    t[2 * i + 1] = (u32)c;
+    c >>= 32;
+  }
+}
+
+// t (< 2^512) mod p: t = H 2^256 + L = L + 977 H + (H << 32) (mod p), twice.
+SECP_HD void fe_reduce(Fe& r, const u32 (&t)[16]) {
+  u32 s[8];
+  u64 c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    u64 x = (u64)t[8 + k] * kP977 + t[k] + c;
+    if (k > 0) x += t[7 + k];
+    s[k] = (u32)x;
+    c = x >> 32;
+  }
+  const u64 top = c + t[15];  // < 2^34
+  const u64 m = top * kP977;
+  u64 x = (u64)s[0] + (u32)m;
+  s[0] = (u32)x;
+  c = x >> 32;
+  x = (u64)s[1] + (m >> 32) + (u32)top + c;
+  s[1] = (u32)x;
+  c = x >> 32;
+  x = (u64)s[2] + (top >> 32) + c;
+  s[2] = (u32)x;
+  c = x >> 32;
+#pragma unroll
+  for (int k = 3; k < 8; ++k) {
+    x = (u64)s[k] + c;
+    s[k] = (u32)x;
+    c = x >> 32;
+  }
+  // a final wrap leaves s tiny (< 2^67): add 2^32 + 977 once more without overflow
+  const u32 w = (u32)c;
+  x = (u64)s[0] + w * kP977;
+  s[0] = (u32)x;
+  x = (x >> 32) + (u64)s[1] + w;
+  s[1] = (u32)x;
+  x = (x >> 32) + (u64)s[2];
+  s[2] = (u32)x;
+  x = (x >> 32) + (u64)s[3];
+  s[3] = (u32)x;
+  fe_canon(r, s);
+}
+
+SECP_HD void fe_mul(Fe& r, const Fe& a, const Fe& b) {
+  u32 t[16];
+  mul_wide(t, a.v, b.v);
+  fe_reduce(r, t);
+}
+SECP_HD void fe_sqr(Fe& r, const Fe& a) {
+  u32 t[16];
+  sqr_wide(t, a.v);
+  fe_reduce(r, t);
+}
+SECP_HD void fe_sqr_n(Fe& r, const Fe& a, int n) {
+  r = a;
+  for (int i = 0; i < n; ++i) fe_sqr(r, r);
+}
+
+// a^((p+1)/4): libsecp256k1's addition chain (x2 .. x223 blocks of ones).
+// r^2 == a iff a is a quadratic residue.
+SECP_HD void fe_pow_sqrt(Fe& r, const Fe& a) {
+  Fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  fe_sqr(x2, a);
+  fe_mul(x2, x2, a);
+  fe_sqr(x3, x2);
+  fe_mul(x3, x3, a);
+  fe_sqr_n(x6, x3, 3);
+  fe_mul(x6, x6, x3);
+  fe_sqr_n(x9, x6, 3);
+  fe_mul(x9, x9, x3);
+  fe_sqr_n(x11, x9, 2);
+  fe_mul(x11, x11, x2);
+  fe_sqr_n(x22, x11, 11);
+  fe_mul(x22, x22, x11);
+  fe_sqr_n(x44, x22, 22);
+  fe_mul(x44, x44, x22);
+  fe_sqr_n(x88, x44, 44);
+  fe_mul(x88, x88, x44);
+  fe_sqr_n(x176, x88, 88);
+  fe_mul(x176, x176, x88);
+  fe_sqr_n(x220, x176, 44);
+  fe_mul(x220, x220, x44);
+  fe_sqr_n(x223, x220, 3);
+  fe_mul(x223, x223, x3);
+  fe_sqr_n(t, x223, 23);
+  fe_mul(t, t, x22);
+  fe_sqr_n(t, t, 6);
+  fe_mul(t, t, x2);
+  fe_sqr(t, t);
+  fe_sqr(r, t);
+}
+
+// a^(p-2) = a^-1 (a != 0): the same chain with the inverse's tail.
+SECP_HD void fe_inv(Fe& r, const Fe& a) {
+  Fe x2, x3, x6, x9, x11, x22, x44, x88, x176, x220, x223, t;
+  fe_sqr(x2, a);
+  fe_mul(x2, x2, a);
+  fe_sqr(x3, x2);
+  fe_mul(x3, x3, a);
+  fe_sqr_n(x6, x3, 3);
+  fe_mul(x6, x6, x3);
+  fe_sqr_n(x9, x6, 3);
+  fe_mul(x9, x9, x3);
+  fe_sqr_n(x11, x9, 2);
+  fe_mul(x11, x11, x2);
+  fe_sqr_n(x22, x11, 11);
+  fe_mul(x22, x22, x11);
+  fe_sqr_n(x44, x22, 22);
+  fe_mul(x44, x44, x22);
+  fe_sqr_n(x88, x44, 44);
+  fe_mul(x88, x88, x44);
+  fe_sqr_n(x176, x88, 88);
+  fe_mul(x176, x176, x88);
+  fe_sqr_n(x220, x176, 44);
+  fe_mul(x220, x220, x44);
+  fe_sqr_n(x223, x220, 3);
+  fe_mul(x223, x223, x3);
+  fe_sqr_n(t, x223, 23);
+  fe_mul(t, t, x22);
+  fe_sqr_n(t, t, 5);
+  fe_mul(t, t, a);
+  fe_sqr_n(t, t, 3);
+  fe_mul(t, t, x2);
+  fe_sqr_n(t, t, 2);
+  fe_mul(r, t, a);
+}
+
+// ---------------------------------------------------------- scalars Z_n
+// C = 2^256 - n (129 bits)
+SECP_HD u32 kC(int j) {
+  return j == 0 ? 0x2FC9BEBFu : j == 1 ? 0x402DA173u : j == 2 ? 0x50B75FC4u : j == 3 ? 0x45512319u : 1u;
+}
+
+// r = a + C mod 2^256; returns the carry out (1 iff a >= n)
+SECP_HD u32 add_c(u32 (&r)[8], const u32 (&a)[8]) {
+  u64 d = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    d += (u64)a[i] + (i < 5 ? kC(i) : 0u);
+    r[i] = (u32)d;
+    d >>= 32;
+  }
+  return (u32)d;
+}
+
+SECP_HD bool sc_ge_n(const u32 (&a)[8]) {
+  u32 t[8];
+  return add_c(t, a) != 0;
+}
+
+// a (< 2^256) -> a mod n
+SECP_HD void sc_canon(Sc& r, const u32 (&a)[8]) {
+  u32 t[8];
+  const u32 ge = add_c(t, a);
+  sel8(r.v, ge != 0, t, a);
+}
+
+// out = in[0..8) + in[8..NI) * C  (NO limbs; the caller's bound keeps it in range)
+template <int NI, int NO>
+SECP_HD void sc_fold(const u32 (&in)[NI], u32 (&out)[NO]) {
+#pragma unroll
+  for (int i = 0; i < NO; ++i) out[i] = i < 8 ? in[i] : 0u;
+#pragma unroll
+  for (int i = 0; i < NI - 8; ++i) {
+    u64 c = 0;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (i + j < NO) {
+        const u64 x = (u64)in[8 + i] * kC(j) + out[i + j] + c;
+        out[i + j] = (u32)x;
+        c = x >> 32;
+      }
+    }
+#pragma unroll
+    for (int k = i + 5; k < NO; ++k) {
+      const u64 x = (u64)out[k] + c;
+      out[k] = (u32)x;
+      c = x >> 32;
+    }
+  }
+}
+
+SECP_HD void sc_reduce(Sc& r, const u32 (&t)[16]) {
+  u32 a[13], b[9], c[9], d[9];
+  sc_fold<16, 13>(t, a);  // < 2^256 + 2^385
+  sc_fold<13, 9>(a, b);   // < 2^256 + 2^259
+  sc_fold<9, 9>(b, c);    // < 2^256 + 2^133
+  sc_fold<9, 9>(c, d);    // < 2^256
+  u32 e[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) e[i] = d[i];
+  sc_canon(r, e);
+}
+
+SECP_HD void sc_mul(Sc& r, const Sc& a, const Sc& b) {
+  u32 t[16];
+  mul_wide(t, a.v, b.v);
+  sc_reduce(r, t);
+}
+
+// a^(n-2) = a^-1 (a != 0).  The exponent is a constant, so the branch on its
+// bits is uniform across the wave.
+SECP_HD void sc_inv(Sc& r, const Sc& a) {
+  // n - 2, little-endian limbs
+  const u32 e[8] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                    0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  Sc x = a;
+  // top bit of n-2 is set: start from a
+  for (int bit = 254; bit >= 0; --bit) {
+    u32 t[16];
+    sqr_wide(t, x.v);
+    sc_reduce(x, t);
+    if ((e[bit >> 5] >> (bit & 31)) & 1u) sc_mul(x, x, a);
+  }
+  r = x;
+}
+
+// ------------------------------------------------------------------ points
+SECP_HD void gej_set_ge(Gej& r, const Ge& a) {
+  r.x = a.x;
+  r.y = a.y;
+  fe_set_u32(r.z, 1);
+  r.inf = 0;
+}
+
+SECP_HD void gej_set_inf(Gej& r) {
+  set_zero(r.x.v);
+  set_zero(r.y.v);
+  set_zero(r.z.v);
+  r.inf = 1;
+}
+
+// 2a  (dbl-2009-l, a = 0: 2M + 5S).  y = 0 cannot occur on secp256k1.
+SECP_HD void gej_double(Gej& r, const Gej& a) {
+  Fe A, B, C, D, E, F, t;
+  fe_sqr(A, a.x);
+  fe_sqr(B, a.y);
+  fe_sqr(C, B);
+  fe_add(t, a.x, B);
+  fe_sqr(t, t);
+  fe_sub(t, t, A);
+  fe_sub(t, t, C);
+  fe_add(D, t, t);
+  fe_add(E, A, A);
+  fe_add(E, E, A);
+  fe_sqr(F, E);
+  Fe z3;
+  fe_mul(z3, a.y, a.z);
+  fe_add(r.z, z3, z3);
+  fe_sub(t, F, D);
+  fe_sub(r.x, t, D);
+  fe_sub(t, D, r.x);
+  fe_mul(t, E, t);
+  fe_add(C, C, C);
+  fe_add(C, C, C);
+  fe_add(C, C, C);
+  fe_sub(r.y, t, C);
+  r.inf = a.inf;
+}
+
+// a + b, b affine  (madd-2007-bl: 7M + 4S); every special case handled.
+SECP_HD void gej_add_ge(Gej& r, const Gej& a, const Ge& b) {
+  if (a.inf) {
+    gej_set_ge(r, b);
+    return;
+  }
+  Fe z1z1, u2, s2, h, hh, i4, j, rr, v, t;
+  fe_sqr(z1z1, a.z);
+  fe_mul(u2, b.x, z1z1);
+  fe_mul(s2, b.y, a.z);
+  fe_mul(s2, s2, z1z1);
+  fe_sub(h, u2, a.x);
+  fe_sub(rr, s2, a.y);
+  if (is_zero8(h.v)) {  // same x: doubling or the point at infinity (rare: branch)
+    if (is_zero8(rr.v)) gej_double(r, a);
+    else gej_set_inf(r);
+    return;
+  }
+  fe_add(rr, rr, rr);
+  fe_sqr(hh, h);
+  fe_add(i4, hh, hh);
+  fe_add(i4, i4, i4);
+  fe_mul(j, h, i4);
+  fe_mul(v, a.x, i4);
+  Fe x3, y3, z3;
+  fe_sqr(x3, rr);
+  fe_sub(x3, x3, j);
+  fe_sub(x3, x3, v);
+  fe_sub(x3, x3, v);
+  fe_sub(t, v, x3);
+  fe_mul(y3, rr, t);
+  fe_mul(t, a.y, j);
+  fe_add(t, t, t);
+  fe_sub(y3, y3, t);
+  fe_add(z3, a.z, h);
+  fe_sqr(z3, z3);
+  fe_sub(z3, z3, z1z1);
+  fe_sub(z3, z3, hh);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+  r.inf = 0;
+}
+
+// a + b, both Jacobian  (add-2007-bl: 11M + 5S); every special case handled.
+SECP_HD void gej_add(Gej& r, const Gej& a, const Gej& b) {
+  if (a.inf) {
+    r = b;
+    return;
+  }
+  if (b.inf) {
+    r = a;
+    return;
+  }
+  Fe z1z1, z2z2, u1, u2, s1, s2, h, i, j, rr, v, t;
+  fe_sqr(z1z1, a.z);
+  fe_sqr(z2z2, b.z);
+  fe_mul(u1, a.x, z2z2);
+  fe_mul(u2, b.x, z1z1);
+  fe_mul(s1, a.y, b.z);
+  fe_mul(s1, s1, z2z2);
+  fe_mul(s2, b.y, a.z);
+  fe_mul(s2, s2, z1z1);
+  fe_sub(h, u2, u1);
+  fe_sub(rr, s2, s1);
+  if (is_zero8(h.v)) {
+    if (is_zero8(rr.v)) gej_double(r, a);
+    else gej_set_inf(r);
+    return;
+  }
+  fe_add(rr, rr, rr);
+  fe_add(i, h, h);
+  fe_sqr(i, i);
+  fe_mul(j, h, i);
+  fe_mul(v, u1, i);
+  Fe x3, y3, z3;
+  fe_sqr(x3, rr);
+  fe_sub(x3, x3, j);
+  fe_sub(x3, x3, v);
+  fe_sub(x3, x3, v);
+  fe_sub(t, v, x3);
+  fe_mul(y3, rr, t);
+  fe_mul(t, s1, j);
+  fe_add(t, t, t);
+  fe_sub(y3, y3, t);
+  fe_add(z3, a.z, b.z);
+  fe_sqr(z3, z3);
+  fe_sub(z3, z3, z1z1);
+  fe_sub(z3, z3, z2z2);
+  fe_mul(z3, z3, h);
+  r.x = x3;
+  r.y = y3;
+  r.z = z3;
+  r.inf = 0;
+}
+
+SECP_HD void gej_to_ge(Ge& r, const Gej& a) {  // a not at infinity
+  Fe zi, zi2, zi3;
+  fe_inv(zi, a.z);
+  fe_sqr(zi2, zi);
+  fe_mul(zi3, zi2, zi);
+  fe_mul(r.x, a.x, zi2);
+  fe_mul(r.y, a.y, zi3);
+}
+
+SECP_HD void ge_generator(Ge& g) {
+  const u32 gx[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                     0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+  const u32 gy[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                     0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    g.x.v[i] = gx[i];
+    g.y.v[i] = gy[i];
+  }
+}
+
+// y^2 == x^3 + 7
+SECP_HD bool ge_on_curve(const Ge& a) {
+  Fe l, r, seven;
+  fe_sqr(l, a.y);
+  fe_sqr(r, a.x);
+  fe_mul(r, r, a.x);
+  fe_set_u32(seven, 7);
+  fe_add(r, r, seven);
+  return eq8(l.v, r.v);
+}
+
+// Compressed-key decompression: y with parity `odd` for x; false if x^3 + 7
+// has no square root (libsecp256k1 set_xo_var).
+SECP_HD bool ge_set_xo(Ge& r, const Fe& x, bool odd) {
+  Fe c, seven, y, y2;
+  fe_sqr(c, x);
+  fe_mul(c, c, x);
+  fe_set_u32(seven, 7);
+  fe_add(c, c, seven);
+  fe_pow_sqrt(y, c);
+  fe_sqr(y2, y);
+  if (!eq8(y2.v, c.v)) return false;
+  if (((y.v[0] & 1u) != 0) != odd) fe_neg(y, y);
+  r.x = x;
+  r.y = y;
+  return true;
+}
+
+// The G table: gtab[256 i + j] = j 2^(8 i) G (affine; j = 0 unused), so
+// u G = sum over the 32 bytes b_i of u of gtab[256 i + b_i] -- 32 mixed
+// additions and no doublings.
+constexpr int kGTabRows = 32;
+constexpr int kGTabEntries = kGTabRows * 256;
+
+// u1 G + u2 Q.  Q part: 4-bit fixed windows over a 15-entry Jacobian table
+// (64 windows: 4 doublings + 1 addition each); G part: the byte table.
+SECP_HD void ecmult(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* gtab) {
+  Gej tbl[15];
+  gej_set_ge(tbl[0], q);
+  gej_double(tbl[1], tbl[0]);
+  for (int i = 2; i < 15; ++i) gej_add_ge(tbl[i], tbl[i - 1], q);
+  Gej acc;
+  gej_set_inf(acc);
+  for (int w = 63; w >= 0; --w) {
+    gej_double(acc, acc);
+    gej_double(acc, acc);
+    gej_double(acc, acc);
+    gej_double(acc, acc);
+    const u32 d = (u2.v[w >> 3] >> (4 * (w & 7))) & 15u;
+    if (d) {
+      Gej t;
+      gej_add(t, acc, tbl[d - 1]);
+      acc = t;
+    }
+  }
+  for (int i = 0; i < kGTabRows; ++i) {
+    const u32 b = (u1.v[i >> 2] >> (8 * (i & 3))) & 255u;
+    if (b) {
+      const Ge g = gtab[256 * i + b];
+      Gej t;
+      gej_add_ge(t, acc, g);
+      acc = t;
+    }
+  }
+  r = acc;
+}
+
+// libsecp256k1 verify_raw: r, s in [1, n); z the message scalar.
+SECP_HD bool ecdsa_verify(const Sc& r, const Sc& s, const Sc& z, const Ge& q, const Ge* gtab) {
+  if (is_zero8(r.v) || is_zero8(s.v)) return false;
+  Sc sn, u1, u2;
+  sc_inv(sn, s);
+  sc_mul(u1, z, sn);
+  sc_mul(u2, r, sn);
+  Gej R;
+  ecmult(R, q, u2, u1, gtab);
+  if (R.inf) return false;
+  // x(R) == r (as field elements, r < n < p) <=> X == r Z^2
+  Fe z2, xr, rz;
+  fe_sqr(z2, R.z);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xr.v[i] = r.v[i];
+  fe_mul(rz, xr, z2);
+  if (eq8(rz.v, R.x.v)) return true;
+  // r + n < p: the x coordinate may have been reduced mod n
+  // p - n = 0x14551231950B75FC4402DA1732FC9BEBE ... compare r < p - n <=> r + n < p
+  u32 t[8];
+  u64 c = 0;
+  const u32 nl[8] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
+                     0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (u64)r.v[i] + nl[i];
+    t[i] = (u32)c;
+    c >>= 32;
+  }
+  if (c || !fe_lt_p(t)) return false;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) xr.v[i] = t[i];
+  fe_mul(rz, xr, z2);
+  return eq8(rz.v, R.x.v);
+}
+
+}  // namespace secp
+}  // namespace dc

@@ -94,6 +94,9 @@ def lib():
         "dc_state_hash": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
         "dc_state_hash_device": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32,
                                            _vp]),
+        "dc_verify_tx_batch": (C.c_int, [_vp, C.c_char_p, _vp, _vp, _vp, C.c_uint32, _vp]),
+        "dc_verify_tx_batch_device": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_uint32, _vp]),
+        "dc_sig_verdict_message": (C.c_char_p, [C.c_uint8]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -141,6 +144,30 @@ def pack_names(pairs):
             blob += name.encode()
             off.append(len(blob))
     return bytes(blob), np.array(off, np.uint32)
+
+
+SIG_OK, SIG_BAD_SIG_HEX, SIG_BAD_SIG, SIG_BAD_PK_HEX, SIG_BAD_PK, SIG_INVALID, SIG_WRONG_OWNER = range(7)
+
+
+def pack_txs(strings, actions, turns=None):
+    """[(white, black, signature_hex, pub_key_hex), ...] + uint32 actions [n, 4]
+    (+ optional int8 turns, -1 = no owner check) -> the dc_verify_tx_batch inputs
+    (utf-8 blob, uint32 offsets [4n+1], actions, turns)."""
+    blob, off = bytearray(), [0]
+    for quad in strings:
+        for s in quad:
+            blob += s.encode()
+            off.append(len(blob))
+    actions = np.ascontiguousarray(actions, np.uint32).reshape(-1, 4)
+    assert len(actions) == len(strings)
+    if turns is not None:
+        turns = np.ascontiguousarray(turns, np.int8)
+        assert len(turns) == len(strings)
+    return bytes(blob), np.array(off, np.uint32), actions, turns
+
+
+def sig_verdict_message(v):
+    return lib().dc_sig_verdict_message(v).decode()
 
 
 def _json_str(text):
@@ -336,6 +363,23 @@ class Engine:
     def state_hash_device(self, d_moves, n_games, n_plies, names_blob, names_off, d_hashes, history=""):
         _check(lib().dc_state_hash_device(self.ctx, None, history.encode(), names_blob, _ptr(names_off), d_moves.ptr,
                                           n_games, n_plies, d_hashes.ptr), "dc_state_hash_device")
+
+    def verify_txs(self, blob, off, actions, turns=None):
+        """App::validate_signature (+ the owner check when turns is given) for a
+        batch of transactions (dc_verify_tx_batch); inputs from pack_txs.
+        Returns uint8 DC_SIG_* verdicts."""
+        n = len(actions)
+        out = np.zeros(n, np.uint8)
+        if n == 0:
+            return out
+        _check(lib().dc_verify_tx_batch(self.ctx, blob, _ptr(off), _ptr(actions), _ptr(turns), n, _ptr(out)),
+               "dc_verify_tx_batch")
+        return out
+
+    def verify_txs_device(self, d_blob, d_off, d_actions, d_turns, n, d_verdicts):
+        _check(lib().dc_verify_tx_batch_device(self.ctx, d_blob.ptr, d_off.ptr, d_actions.ptr,
+                                               d_turns.ptr if d_turns else None, n, d_verdicts.ptr),
+               "dc_verify_tx_batch_device")
 
     def gen_games(self, seed, first_game, n_games, n_plies, noise_per_256=32, rules=RULES_REF):
         out = np.zeros((n_plies, n_games), np.uint16)

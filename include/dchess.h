@@ -208,6 +208,36 @@ int dc_state_hash_device(dc_ctx* ctx, const dc_pos* start, const char* history, 
                          const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
                          uint8_t* d_hashes);
 
+/* ---------------------------------------------------- transaction signatures
+ * The other per-transaction check of is_valid_tx (core/src/consensus/hotstuff.rs:139):
+ * App::validate_signature (hotstuff.rs:168-208), batched on the GPU.  Per
+ * transaction i:
+ *   strings[str_off[4i+0] .. str_off[4i+1])  white_player (UTF-8)
+ *   strings[str_off[4i+1] .. str_off[4i+2])  black_player
+ *   strings[str_off[4i+2] .. str_off[4i+3])  signature (hex text, 64 bytes r||s)
+ *   strings[str_off[4i+3] .. str_off[4i+4])  pub_key (hex text: 33, 64 or 65 bytes)
+ *   actions[4i .. 4i+4) = action[0].x, action[0].y, action[1].x, action[1].y
+ *   turns[i] (optional; NULL or -1 = skip) = the game's turn: after a valid
+ *   signature, pub_key must equal the string of the player to move
+ *   (hotstuff.rs:141-148), else DC_SIG_WRONG_OWNER.
+ * The signed message is serde_json {"whitePlayer","blackPlayer","action":[{x,y},{x,y}]}
+ * (hotstuff.rs:169-179), hashed with SHA-256; verification follows
+ * libsecp256k1 0.7.1 (Message mod n, parse_standard_slice, parse_slice,
+ * verify without a low-s rule).  Verdicts in the reference's check order: */
+#define DC_SIG_OK 0
+#define DC_SIG_BAD_SIG_HEX 1  /* hex::decode(signature) failed            hotstuff.rs:183-184 */
+#define DC_SIG_BAD_SIG 2      /* Signature::parse_standard_slice failed    hotstuff.rs:186-191 */
+#define DC_SIG_BAD_PK_HEX 3   /* hex::decode(pub_key) failed               hotstuff.rs:193-194 */
+#define DC_SIG_BAD_PK 4       /* PublicKey::parse_slice failed             hotstuff.rs:195-200 */
+#define DC_SIG_INVALID 5      /* verify() false: "invalid signature"       hotstuff.rs:202-206 */
+#define DC_SIG_WRONG_OWNER 6  /* pub_key is not the mover: "invalud turn"  hotstuff.rs:141-148 */
+int dc_verify_tx_batch(dc_ctx* ctx, const char* strings, const uint32_t* str_off, const uint32_t* actions,
+                       const int8_t* turns, uint32_t n, uint8_t* verdicts);
+int dc_verify_tx_batch_device(dc_ctx* ctx, const char* d_strings, const uint32_t* d_str_off,
+                              const uint32_t* d_actions, const int8_t* d_turns, uint32_t n, uint8_t* d_verdicts);
+/* Text for a DC_SIG_* verdict ("" for OK; codes 5 and 6 are the reference's strings). */
+const char* dc_sig_verdict_message(uint8_t verdict);
+
 /* -------------------------------------------------------------------- perft
  * perft(pos, depth) = number of leaf nodes of the move tree (under
  * REF the tree is every (from,to) pair validate_move accepts).  divide[i] is the
