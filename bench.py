@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--no-perft", action="store_true", help="with --profile-only: replay leg only (PMC passes)")
     ap.add_argument("--hash-games", type=int, default=1_000_000, help="state-hash leg: games per rank (0: off)")
     ap.add_argument("--hash-steps", type=int, default=3)
+    ap.add_argument("--txs", type=int, default=262_144, help="signature leg: transactions per rank (0: off)")
+    ap.add_argument("--tx-steps", type=int, default=3)
     return ap.parse_args()
 
 
@@ -289,6 +291,84 @@ def state_hash_leg(eng, d, args):
             "first_hash": "0x" + bytes(h0).hex()}
 
 
+def txsig_leg(eng, d, args):
+    """App::validate_signature (core/src/consensus/hotstuff.rs:168-208) + the owner
+    check (:141-148) for a resident batch: the 512 signed transactions of
+    tests/golden/txsig_batch.json tiled to --txs, parity-checked against the
+    fixture's verdicts (dc_verify_tx_batch_device, k_verify_tx)."""
+    fx = json.load(open(os.path.join(REPO, "tests", "golden", "txsig_batch.json")))["txs"]
+    n = args.txs
+    reps = (n + len(fx) - 1) // len(fx)
+    blob, off, acts, turns = dchess.pack_txs([(t["white"], t["black"], t["sig"], t["pk"]) for t in fx] * reps,
+                                             np.array([t["action"] for t in fx] * reps, np.uint32),
+                                             np.array([t["turn"] for t in fx] * reps, np.int8))
+    off, acts, turns = off[:4 * n + 1], acts[:n], turns[:n]
+    blob = blob[:int(off[-1])]
+    want = np.array([t["verdict"] for t in fx] * reps, np.uint8)[:n]
+    bufs = []
+    for arr in (np.frombuffer(blob, np.uint8), off, acts, turns):
+        b = eng.alloc(max(arr.nbytes, 1))
+        b.upload(arr)
+        bufs.append(b)
+    d_v = eng.alloc(n)
+    eng.verify_txs_device(*bufs, n, d_v)  # warmup (builds the G table once per context)
+    got = d_v.download(np.uint8, n)
+    if not (got == want).all():
+        raise SystemExit(f"parity failure: {int((got != want).sum())} signature verdicts differ from the fixture")
+    d.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.tx_steps):
+        eng.verify_txs_device(*bufs, n, d_v)
+    d.sync()
+    dt = d.max(time.perf_counter() - t0)
+    eng.reset_stats()
+    eng.set_profiling(True)
+    eng.verify_txs_device(*bufs, n, d_v)
+    eng.set_profiling(False)
+    k = eng.kernel_stats("verify_tx")
+    for b in bufs + [d_v]:
+        b.free()
+    kms = k["total_ms"] / max(k["launches"], 1)
+    out = {"value": n * d.world * args.tx_steps / dt, "unit": "transaction signature checks/s", "scaling": "weak",
+           "workload": f"{n} transactions per rank (512 distinct client-signed txs tiled; compressed secp256k1 keys; "
+                       "26 % rejected): serde_json message + SHA-256 + hex/key parse + ECDSA verify + owner check",
+           "ms_per_step": 1e3 * dt / args.tx_steps, "kernel_avg_ms": kms, "kernel_per_s": n / (kms / 1e3)}
+    rec = _pmc("verify_tx")
+    if rec and d.world == 1:
+        w = rec["valu_lane_ops_per_unit"]
+        out["roofline"] = {"bound": "valu", "kernel": "k_verify_tx", "unit": "TOPS (int32 VALU lane-ops/s)",
+                           "achieved": n / (kms / 1e3) * w / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+                           "W_lane_ops_per_tx": w, "W_source": rec["source"],
+                           "frac": n / (kms / 1e3) * w / VALU_PEAK_LANE_OPS}
+    return out
+
+
+def cpu_txsig(threads):
+    """The same per-transaction code compiled for the host (build/test_secp, the
+    kernel's dc_txsig.h on one core) over a bounded sample of the fixture."""
+    import subprocess
+    exe = os.path.join(REPO, "distributed-chess_amd", "build", "test_secp")
+    if not os.path.exists(exe):
+        return None
+    fx = json.load(open(os.path.join(REPO, "tests", "golden", "txsig_batch.json")))["txs"][:256]
+    h = lambda s: s.encode().hex() or "-"  # noqa: E731
+    lines = "".join(f"tx {h(t['white'])} {h(t['black'])} {' '.join(map(str, t['action']))} {h(t['sig'])} "
+                    f"{h(t['pk'])} {t['turn']}\n" for t in fx)
+    p = subprocess.run([exe], input="mulg 01\n", capture_output=True, text=True, timeout=120)  # G table only
+    t0 = time.perf_counter()
+    p = subprocess.run([exe], input="mulg 01\n" + lines, capture_output=True, text=True, timeout=300)
+    dt = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    subprocess.run([exe], input="mulg 01\n", capture_output=True, text=True, timeout=120)
+    dt -= time.perf_counter() - t0  # minus the G-table build
+    got = [int(x) for x in p.stdout.split()[2:]]
+    if got != [t["verdict"] for t in fx]:
+        raise SystemExit("parity failure: host build of k_verify_tx's code disagrees with the fixture")
+    return {"value": len(fx) / dt, "unit": "transaction signature checks/s", "cores": 1, "kind": "port",
+            "sample": f"host build of dc_txsig.h (clang -O2, 32-bit limbs) over {len(fx)} fixture transactions on one "
+                      "core; the reference's libsecp256k1 could not be built here"}
+
+
 def main():
     args = parse()
     d = Dist(args.gpus)
@@ -350,6 +430,11 @@ def main():
     if args.hash_games > 0 and not args.profile_only:
         shash = state_hash_leg(eng, d, args)
 
+    # ------------------------------------ transaction signatures
+    txsig = None
+    if args.txs > 0 and (not args.profile_only or args.no_perft):
+        txsig = txsig_leg(eng, d, args)
+
     if d.rank != 0 or args.profile_only:
         return
     line = {
@@ -371,9 +456,15 @@ def main():
         line["state_hash"] = shash
     if replay is not None:
         line["replay"] = replay
+    if txsig is not None:
+        line["tx_signatures"] = txsig
     if not args.no_cpu and d.world == 1:
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         line.update(cpu_baselines(args, threads))
+        if txsig is not None:
+            ct = cpu_txsig(threads)
+            if ct is not None:
+                line["tx_signatures"]["cpu_baseline"] = ct
     print(json.dumps(line), flush=True)
 
 

@@ -54,4 +54,20 @@ a = json.load(open("gpurun_out/pmc_perft.json")); a.update(json.load(open("gpuru
 json.dump(a, open("gpurun_out/pmc_latest.json", "w"), indent=1)
 PY
 fi
+if has txpmc; then
+  rm -rf $O/pmc_t*
+  P="--steps 1 --warmup 0 --no-cpu --profile-only --no-perft --no-replay --tx-steps 1"
+  tpass() { local c=$1 t=$2; step "pmc $t"; timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err; }
+  tpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" t1 && \
+  tpass "FETCH_SIZE" t2 && tpass "WRITE_SIZE" t3 && tpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" t4 && tpass "VALUBusy" t5 || { tail $O/pmc.err; exit 7; }
+  mkdir -p $O/tx && mv $O/pmc_t[1-5] $O/tx/
+  python tools/pmc_summary.py $O/tx --json $O/pmc_tx.json --tx-units 262144 --source "rocprofv3 --pmc, bench.py $P" > $O/pmc_tx.txt
+  python - <<'PY'
+import json, os
+p = "gpurun_out/pmc_latest.json"
+a = json.load(open(p)) if os.path.exists(p) else json.load(open("profiles/pmc_latest.json"))
+a.update(json.load(open("gpurun_out/pmc_tx.json")))
+json.dump(a, open(p, "w"), indent=1)
+PY
+fi
 step done

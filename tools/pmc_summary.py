@@ -15,6 +15,7 @@ ap.add_argument("root", nargs="?", default="gpurun_out")
 ap.add_argument("--json")
 ap.add_argument("--depth", type=int, default=7)
 ap.add_argument("--replay-units", type=float, default=0.0, help="validated moves per replay dispatch")
+ap.add_argument("--tx-units", type=float, default=0.0, help="transactions per k_verify_tx dispatch")
 ap.add_argument("--source", default="")
 a = ap.parse_args()
 REF = {6: 120909581, 7: 3282734510}
@@ -53,5 +54,9 @@ if a.json:
             out["replay"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
                              "valu_lane_ops_per_move": c.get("SQ_INSTS_VALU", 0) * 64 / a.replay_units,
                              "counters_per_dispatch": c, "source": a.source}
+        if "k_verify_tx" in k and a.tx_units:
+            out["verify_tx"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
+                                "valu_lane_ops_per_unit": c.get("SQ_INSTS_VALU", 0) * 64 / a.tx_units,
+                                "counters_per_dispatch": c, "source": a.source}
     json.dump(out, open(a.json, "w"), indent=1)
     print("wrote", a.json)
