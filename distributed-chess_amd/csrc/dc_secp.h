@@ -87,20 +87,35 @@ SECP_HD void to_be32(const u32 (&a)[8], uint8_t* b) {
 // ------------------------------------------------------------- field F_p
 constexpr u32 kP977 = 977u;
 
+// 32-bit add/subtract with carry: v_add_co / v_addc_co chains on the device
+// (a u64 formulation costs a zero-extension v_mov per limb).
+SECP_HD u32 addc32(u32 x, u32 y, u32 cin, u32* cout) {
+#if defined(__clang__)
+  return __builtin_addc(x, y, cin, cout);
+#else
+  const u64 d = (u64)x + y + cin;
+  *cout = (u32)(d >> 32);
+  return (u32)d;
+#endif
+}
+SECP_HD u32 subb32(u32 x, u32 y, u32 bin, u32* bout) {
+#if defined(__clang__)
+  return __builtin_subc(x, y, bin, bout);
+#else
+  const u64 d = (u64)x - y - bin;
+  *bout = (u32)(d >> 63);
+  return (u32)d;
+#endif
+}
+
 // r = a + (2^32 + 977) mod 2^256; returns the carry out (1 iff a >= p).
 SECP_HD u32 add_k(u32 (&r)[8], const u32 (&a)[8]) {
-  u64 d = (u64)a[0] + kP977;
-  r[0] = (u32)d;
-  d = (d >> 32) + (u64)a[1] + 1u;
-  r[1] = (u32)d;
-  d >>= 32;
+  u32 c;
+  r[0] = addc32(a[0], kP977, 0u, &c);
+  r[1] = addc32(a[1], 1u, c, &c);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    d += a[i];
-    r[i] = (u32)d;
-    d >>= 32;
-  }
-  return (u32)d;
+  for (int i = 2; i < 8; ++i) r[i] = addc32(a[i], 0u, c, &c);
+  return c;
 }
 
 SECP_HD bool fe_lt_p(const u32 (&a)[8]) {
@@ -121,42 +136,24 @@ SECP_HD void fe_set_u32(Fe& r, u32 x) {
 }
 
 SECP_HD void fe_add(Fe& r, const Fe& a, const Fe& b) {
-  u32 s[8], t[8];
-  u64 c = 0;
+  u32 s[8], t[8], c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c += (u64)a.v[i] + b.v[i];
-    s[i] = (u32)c;
-    c >>= 32;
-  }
+  for (int i = 0; i < 8; ++i) s[i] = addc32(a.v[i], b.v[i], c, &c);
   // a + b < 2p: if it overflowed 2^256 or s >= p, the result is s + (2^256 - p)
   const u32 d = add_k(t, s);
   sel8(r.v, (c | d) != 0, t, s);
 }
 
 SECP_HD void fe_sub(Fe& r, const Fe& a, const Fe& b) {
-  u32 s[8];
-  u64 br = 0;
+  u32 s[8], br = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const u64 t = (u64)a.v[i] - b.v[i] - br;
-    s[i] = (u32)t;
-    br = (t >> 32) & 1u;
-  }
+  for (int i = 0; i < 8; ++i) s[i] = subb32(a.v[i], b.v[i], br, &br);
   // borrow: add p, i.e. subtract 2^32 + 977 modulo 2^256
-  const u32 m = (u32)br;
-  u64 t = (u64)s[0] - (m * kP977);
-  r.v[0] = (u32)t;
-  u64 b2 = (t >> 32) & 1u;
-  t = (u64)s[1] - m - b2;
-  r.v[1] = (u32)t;
-  b2 = (t >> 32) & 1u;
+  u32 b2;
+  r.v[0] = subb32(s[0], br * kP977, 0u, &b2);
+  r.v[1] = subb32(s[1], br, b2, &b2);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    t = (u64)s[i] - b2;
-    r.v[i] = (u32)t;
-    b2 = (t >> 32) & 1u;
-  }
+  for (int i = 2; i < 8; ++i) r.v[i] = subb32(s[i], 0u, b2, &b2);
 }
 
 SECP_HD void fe_neg(Fe& r, const Fe& a) {
@@ -165,8 +162,41 @@ SECP_HD void fe_neg(Fe& r, const Fe& a) {
   fe_sub(r, z, a);
 }
 
-// 512-bit product a * b (operand scanning; each step a*b + t + c < 2^64)
+#if defined(__HIP_DEVICE_COMPILE__)
+// gfx950: acc (64 bits) += a * b, the carry out of bit 64 added into hi.  The
+// carry comes from v_mad_u64_u32's VOP3b carry-out (an SGPR lane mask), which C
+// cannot name: 2 VALU per partial product, where the operand-scanned C form
+// costs ~6 (the u64 zero extensions are v_mov; tools/ubench/mul_rate.hip).
+__device__ __forceinline__ void mac_c(u64& acc, u32& hi, u32 a, u32 b) {
+  u64 cc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %0\n\tv_addc_co_u32_e64 %2, %1, %2, 0, %1"
+      : "+v"(acc), "=&s"(cc), "+v"(hi)
+      : "v"(a), "v"(b));
+}
+// acc + x (no carry out of bit 64 possible at the call sites): one v_mad_u64_u32
+// by 1 instead of a zero-extension v_mov plus a 64-bit add.
+__device__ __forceinline__ u64 mad1(u64 acc, u32 x) {
+  u64 cc;
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %0" : "+v"(acc), "=s"(cc) : "v"(x));
+  return acc;
+}
+#endif
+
+// 512-bit product a * b.  Device: product scanning (Comba) on a 96-bit column
+// accumulator; host: operand scanning (each step a*b + t + c < 2^64).
 SECP_HD void mul_wide(u32 (&t)[16], const u32 (&a)[8], const u32 (&b)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  u64 acc = 0;
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    u32 hi = 0;
+#pragma unroll
+    for (int i = (k < 8 ? 0 : k - 7); i <= (k < 8 ? k : 7); ++i) mac_c(acc, hi, a[i], b[k - i]);
+    t[k] = (u32)acc;
+    acc = (acc >> 32) | ((u64)hi << 32);
+  }
+  t[15] = (u32)acc;
+#else
 #pragma unroll
   for (int i = 0; i < 16; ++i) t[i] = 0;
 #pragma unroll
@@ -180,10 +210,29 @@ SECP_HD void mul_wide(u32 (&t)[16], const u32 (&a)[8], const u32 (&b)[8]) {
     }
     t[i + 8] = (u32)c;
   }
+#endif
 }
 
-// 512-bit square: cross products once, doubled, plus the diagonal
+// 512-bit square.  Device: Comba with each cross product accumulated twice
+// (no 97-bit doubling step); host: cross products once, doubled, plus the diagonal.
 SECP_HD void sqr_wide(u32 (&t)[16], const u32 (&a)[8]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  u64 acc = 0;
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    u32 hi = 0;
+#pragma unroll
+    for (int i = (k < 8 ? 0 : k - 7); 2 * i < k; ++i) {
+      mac_c(acc, hi, a[i], a[k - i]);
+      mac_c(acc, hi, a[i], a[k - i]);
+    }
+    if ((k & 1) == 0) mac_c(acc, hi, a[k >> 1], a[k >> 1]);
+    t[k] = (u32)acc;
+    acc = (acc >> 32) | ((u64)hi << 32);
+  }
+  t[15] = (u32)acc;
+  return;
+#endif
 #pragma unroll
   for (int i = 0; i < 16; ++i) t[i] = 0;
 #pragma unroll
@@ -223,6 +272,18 @@ SECP_HD void sqr_wide(u32 (&t)[16], const u32 (&a)[8]) {
 SECP_HD void fe_reduce(Fe& r, const u32 (&t)[16]) {
   u32 s[8];
   u64 c = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // each 32-bit addend is one v_mad_u64_u32 by 1 into the 64-bit column (< 2^43)
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    c = (u64)t[8 + k] * kP977 + c;
+    c = mad1(c, t[k]);
+    if (k > 0) c = mad1(c, t[7 + k]);
+    s[k] = (u32)c;
+    c >>= 32;
+  }
+  const u64 top = mad1(c, t[15]);  // < 2^34
+#else
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     u64 x = (u64)t[8 + k] * kP977 + t[k] + c;
@@ -231,32 +292,26 @@ SECP_HD void fe_reduce(Fe& r, const u32 (&t)[16]) {
     c = x >> 32;
   }
   const u64 top = c + t[15];  // < 2^34
+#endif
+  // + top (2^32 + 977): two carry chains; the sum is < 2^256 + 2^67, so a
+  // carry out leaves s < 2^67 and one more (2^32 + 977) cannot overflow
   const u64 m = top * kP977;
-  u64 x = (u64)s[0] + (u32)m;
-  s[0] = (u32)x;
-  c = x >> 32;
-  x = (u64)s[1] + (m >> 32) + (u32)top + c;
-  s[1] = (u32)x;
-  c = x >> 32;
-  x = (u64)s[2] + (top >> 32) + c;
-  s[2] = (u32)x;
-  c = x >> 32;
+  u32 c1, c2;
+  s[0] = addc32(s[0], (u32)m, 0u, &c1);
+  s[1] = addc32(s[1], (u32)(m >> 32), c1, &c1);
+  s[1] = addc32(s[1], (u32)top, 0u, &c2);
+  s[2] = addc32(s[2], (u32)(top >> 32), c2, &c2);
+  s[2] = addc32(s[2], 0u, c1, &c1);
 #pragma unroll
   for (int k = 3; k < 8; ++k) {
-    x = (u64)s[k] + c;
-    s[k] = (u32)x;
-    c = x >> 32;
+    s[k] = addc32(s[k], 0u, c1, &c1);
+    s[k] = addc32(s[k], 0u, c2, &c2);
   }
-  // a final wrap leaves s tiny (< 2^67): add 2^32 + 977 once more without overflow
-  const u32 w = (u32)c;
-  x = (u64)s[0] + w * kP977;
-  s[0] = (u32)x;
-  x = (x >> 32) + (u64)s[1] + w;
-  s[1] = (u32)x;
-  x = (x >> 32) + (u64)s[2];
-  s[2] = (u32)x;
-  x = (x >> 32) + (u64)s[3];
-  s[3] = (u32)x;
+  const u32 w = c1 + c2;
+  s[0] = addc32(s[0], w * kP977, 0u, &c1);
+  s[1] = addc32(s[1], w, c1, &c1);
+  s[2] = addc32(s[2], 0u, c1, &c1);
+  s[3] = addc32(s[3], 0u, c1, &c1);
   fe_canon(r, s);
 }
 
@@ -352,14 +407,10 @@ SECP_HD u32 kC(int j) {
 
 // r = a + C mod 2^256; returns the carry out (1 iff a >= n)
 SECP_HD u32 add_c(u32 (&r)[8], const u32 (&a)[8]) {
-  u64 d = 0;
+  u32 c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    d += (u64)a[i] + (i < 5 ? kC(i) : 0u);
-    r[i] = (u32)d;
-    d >>= 32;
-  }
-  return (u32)d;
+  for (int i = 0; i < 8; ++i) r[i] = addc32(a[i], i < 5 ? kC(i) : 0u, c, &c);
+  return c;
 }
 
 SECP_HD bool sc_ge_n(const u32 (&a)[8]) {
