@@ -485,6 +485,82 @@ SECP_HD void sc_inv(Sc& r, const Sc& a) {
   r = x;
 }
 
+// (a + b) mod n
+SECP_HD void sc_add(Sc& r, const Sc& a, const Sc& b) {
+  u32 s[8], t[8], c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = addc32(a.v[i], b.v[i], c, &c);
+  const u32 d = add_c(t, s);
+  sel8(r.v, (c | d) != 0, t, s);
+}
+
+// ---------------------------------------------------- GLV endomorphism
+// lambda (Q.x, Q.y) = (beta Q.x, Q.y) with lambda^3 = 1 mod n, beta^3 = 1 mod p.
+// libsecp256k1's scalar_split_lambda: k = r1 + lambda r2 (mod n) with
+// |r1|, |r2| < 2^128, from c_i = round(k g_i / 2^384) and the short lattice
+// basis (b1, b2).  Constants checked in tests/test_txsig.py
+// (test_glv_constants): lambda^3 = 1, beta^3 = 1, lambda G = (beta Gx, Gy),
+// g_i = round(2^384 b_i / n).
+SECP_HD void fe_beta(Fe& r) {
+  const u32 b[8] = {0x719501EEu, 0xC1396C28u, 0x12F58995u, 0x9CF04975u, 0xAC3434E9u, 0x6E64479Eu, 0x657C0710u, 0x7AE96A2Bu};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.v[i] = b[i];
+}
+
+// round(k g / 2^384) (< 2^128 + 1)
+SECP_HD void sc_mul_shift384(Sc& r, const Sc& k, const u32 (&g)[8]) {
+  u32 t[16];
+  mul_wide(t, k.v, g);
+  u32 c = t[11] >> 31;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r.v[i] = addc32(t[12 + i], 0u, c, &c);
+  r.v[4] = c;
+  r.v[5] = r.v[6] = r.v[7] = 0;
+}
+
+SECP_HD void sc_split_lambda(Sc& r1, Sc& r2, const Sc& k) {
+  const u32 g1[8] = {0x45DBB031u, 0xE893209Au, 0x71E8CA7Fu, 0x3DAA8A14u, 0x9284EB15u, 0xE86C90E4u, 0xA7D46BCDu, 0x3086D221u};
+  const u32 g2[8] = {0x8AC47F71u, 0x1571B4AEu, 0x9DF506C6u, 0x221208ACu, 0x0ABFE4C4u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u};
+  Sc mb1, mb2, ml, c1, c2;
+  const u32 vb1[8] = {0x0ABFE4C3u, 0x6F547FA9u, 0x010E8828u, 0xE4437ED6u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u};
+  const u32 vb2[8] = {0x3DB1562Cu, 0xD765CDA8u, 0x0774346Du, 0x8A280AC5u, 0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+  const u32 vml[8] = {0xB51283CFu, 0xE0CFC810u, 0x8EC739C2u, 0xA880B9FCu, 0x77ED9BA4u, 0x5AD9E3FDu, 0x3FA3CF1Fu, 0xAC9C52B3u};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    mb1.v[i] = vb1[i];
+    mb2.v[i] = vb2[i];
+    ml.v[i] = vml[i];
+  }
+  sc_mul_shift384(c1, k, g1);
+  sc_mul_shift384(c2, k, g2);
+  sc_mul(c1, c1, mb1);
+  sc_mul(c2, c2, mb2);
+  sc_add(r2, c1, c2);
+  sc_mul(r1, r2, ml);
+  sc_add(r1, r1, k);
+}
+
+// r (mod n) with |r| < 2^128 as sign + 128-bit magnitude (limbs 0..3)
+SECP_HD bool sc_signed128(u32 (&m)[4], const Sc& r) {
+  const bool neg = (r.v[4] | r.v[5] | r.v[6] | r.v[7]) != 0;
+  const u32 nl[4] = {0xD0364141u, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u};
+  u32 b = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const u32 d = subb32(nl[i], r.v[i], b, &b);  // n - r (its high limbs cancel)
+    m[i] = neg ? d : r.v[i];
+  }
+  return neg;
+}
+
+// radix-16 Booth digit w (0..32) of a 128-bit magnitude: in [-8, 8], no carries:
+// d_w = b[4w..4w+3] + b[4w-1] - 16 b[4w+3]
+SECP_HD int booth16(const u32 (&m)[4], int w) {
+  const u32 lo = w < 32 ? (m[w >> 3] >> (4 * (w & 7))) & 15u : 0u;
+  const u32 below = w > 0 ? (m[(w - 1) >> 3] >> (4 * ((w - 1) & 7) + 3)) & 1u : 0u;
+  return (int)(lo + below) - (int)((lo & 8u) << 1);
+}
+
 // ------------------------------------------------------------------ points
 SECP_HD void gej_set_ge(Gej& r, const Ge& a) {
   r.x = a.x;
@@ -679,25 +755,58 @@ SECP_HD bool ge_set_xo(Ge& r, const Fe& x, bool odd) {
 constexpr int kGTabRows = 32;
 constexpr int kGTabEntries = kGTabRows * 256;
 
-// u1 G + u2 Q.  Q part: 4-bit fixed windows over a 15-entry Jacobian table
-// (64 windows: 4 doublings + 1 addition each); G part: the byte table.
+// u1 G + u2 Q.  Q part: GLV (u2 = k1 + lambda k2, |k_i| < 2^128), radix-16
+// Booth digits over an 8-entry Jacobian table of Q's multiples, lambda applied
+// per lookup as beta X: 128 doublings and 66 additions instead of 256 and 64.
+// G part: the byte table (32 mixed additions, no doublings).
+struct Gj3 {  // Jacobian point known not to be infinity
+  Fe x, y, z;
+};
 SECP_HD void ecmult(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* gtab) {
-  Gej tbl[15];
-  gej_set_ge(tbl[0], q);
-  gej_double(tbl[1], tbl[0]);
-  for (int i = 2; i < 15; ++i) gej_add_ge(tbl[i], tbl[i - 1], q);
+  Sc k1, k2;
+  sc_split_lambda(k1, k2, u2);
+  u32 m1[4], m2[4];
+  const bool n1 = sc_signed128(m1, k1), n2 = sc_signed128(m2, k2);
+  Gj3 tbl[8];  // tbl[i] = (i + 1) Q
+  {
+    Gej t, a;
+    gej_set_ge(a, q);
+    tbl[0] = {a.x, a.y, a.z};
+    gej_double(t, a);
+    tbl[1] = {t.x, t.y, t.z};
+    for (int i = 2; i < 8; ++i) {
+      gej_add_ge(a, t, q);
+      tbl[i] = {a.x, a.y, a.z};
+      t = a;
+    }
+  }
+  Fe beta;
+  fe_beta(beta);
   Gej acc;
   gej_set_inf(acc);
-  for (int w = 63; w >= 0; --w) {
-    gej_double(acc, acc);
-    gej_double(acc, acc);
-    gej_double(acc, acc);
-    gej_double(acc, acc);
-    const u32 d = (u2.v[w >> 3] >> (4 * (w & 7))) & 15u;
-    if (d) {
-      Gej t;
-      gej_add(t, acc, tbl[d - 1]);
-      acc = t;
+  for (int w = 32; w >= 0; --w) {
+    if (w < 32) {
+      gej_double(acc, acc);
+      gej_double(acc, acc);
+      gej_double(acc, acc);
+      gej_double(acc, acc);
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int d = booth16(h ? m2 : m1, w);
+      if (d) {
+        const Gj3& e = tbl[(d < 0 ? -d : d) - 1];
+        Gej p;
+        p.x = e.x;
+        p.y = e.y;
+        p.z = e.z;
+        p.inf = 0;
+        if (h) fe_mul(p.x, p.x, beta);
+        if ((d < 0) != (h ? n2 : n1)) fe_neg(p.y, p.y);
+        Gej t;
+        gej_add(t, acc, p);
+        acc = t;
+      }
     }
   }
   for (int i = 0; i < kGTabRows; ++i) {

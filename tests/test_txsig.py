@@ -98,6 +98,32 @@ def test_oracle_curve_facts():
     assert T.P == 2 ** 256 - 2 ** 32 - 977
 
 
+LAMBDA = 0x5363AD4CC05C30E0A5261C028812645A122E22EA20816678DF02967C1B23BD72
+BETA = 0x7AE96A2B657C07106E64479EAC3434E99CF0497512F58995C1396C28719501EE
+
+
+def test_glv_constants():
+    """The endomorphism constants dc_secp.h's ecmult uses (sc_split_lambda, fe_beta)."""
+    assert pow(LAMBDA, 3, T.N) == 1 and pow(BETA, 3, T.P) == 1
+    assert T.mul(LAMBDA, T.G) == (BETA * T.GX % T.P, T.GY)
+    a1, b1 = 0x3086D221A7D46BCDE86C90E49284EB15, -0xE4437ED6010E88286F547FA90ABFE4C3
+    a2, b2 = 0x114CA50F7A8E2F3F657C1108D9D44CFD8, a1
+    assert (a1 + b1 * LAMBDA) % T.N == 0 and (a2 + b2 * LAMBDA) % T.N == 0
+    g1 = (2 ** 384 * b2 + T.N // 2) // T.N
+    g2 = (2 ** 384 * -b1 + T.N // 2) // T.N
+    assert g1 == 0x3086D221A7D46BCDE86C90E49284EB153DAA8A1471E8CA7FE893209A45DBB031
+    assert g2 == 0xE4437ED6010E88286F547FA90ABFE4C4221208AC9DF506C61571B4AE8AC47F71
+    rng = random.Random(9)
+    for k in [0, 1, T.N - 1, LAMBDA, T.N // 2] + [rng.randrange(T.N) for _ in range(2000)]:
+        c1 = (k * g1 + 2 ** 383) >> 384
+        c2 = (k * g2 + 2 ** 383) >> 384
+        r2 = (c1 * -b1 + c2 * -b2) % T.N
+        r1 = (k - r2 * LAMBDA) % T.N
+        assert (r1 + LAMBDA * r2) % T.N == k
+        for r in (r1, r2):
+            assert min(r, T.N - r) < 2 ** 128
+
+
 def test_oracle_message_json():
     # serde_json with preserve_order: keys in json! order, no whitespace
     assert T.message_json("ab", "cd", (1, 0, 3, 0)) == \
@@ -161,7 +187,10 @@ def test_host_field_scalar_ops(secp_bin):
 
 def test_host_point_mul(secp_bin):
     rng = random.Random(5)
-    for k in [1, 2, 3, 255, 256, T.N - 1, 2 ** 200 + 12345] + [rng.randrange(1, T.N) for _ in range(6)]:
+    # GLV edge scalars: lambda, -lambda, 2^128 +- 1, n / 2, large negative split parts
+    edge = [LAMBDA, T.N - LAMBDA, 2 ** 128 - 1, 2 ** 128, 2 ** 128 + 1, T.N // 2, T.N // 2 + 1, T.N - 2 ** 127,
+            (2 ** 127 + LAMBDA * (2 ** 127 - 1)) % T.N]
+    for k in [1, 2, 3, 255, 256, T.N - 1, 2 ** 200 + 12345] + edge + [rng.randrange(1, T.N) for _ in range(12)]:
         x, y = T.mul(k, T.G)
         assert secp_bin(f"mulg {_h(k)}") == f"{_h(x)} {_h(y)}"
         q = T.mul(rng.randrange(1, T.N), T.G)
