@@ -428,6 +428,23 @@ SECP_HD void sc_canon(Sc& r, const u32 (&a)[8]) {
 // out = in[0..8) + in[8..NI) * C  (NO limbs; the caller's bound keeps it in range)
 template <int NI, int NO>
 SECP_HD void sc_fold(const u32 (&in)[NI], u32 (&out)[NO]) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // product scanning on the 96-bit column accumulator (mac_c), as mul_wide
+  u64 acc = 0;
+#pragma unroll
+  for (int k = 0; k < NO; ++k) {
+    u32 hi = 0;
+    if (k < 8) acc = mad1(acc, in[k]);
+#pragma unroll
+    for (int i = 0; i < NI - 8; ++i) {
+      const int j = k - i;
+      if (j >= 0 && j < 5) mac_c(acc, hi, in[8 + i], kC(j));
+    }
+    out[k] = (u32)acc;
+    acc = (acc >> 32) | ((u64)hi << 32);
+  }
+  return;
+#endif
 #pragma unroll
   for (int i = 0; i < NO; ++i) out[i] = i < 8 ? in[i] : 0u;
 #pragma unroll
@@ -468,19 +485,30 @@ SECP_HD void sc_mul(Sc& r, const Sc& a, const Sc& b) {
   sc_reduce(r, t);
 }
 
-// a^(n-2) = a^-1 (a != 0).  The exponent is a constant, so the branch on its
-// bits is uniform across the wave.
+// a^(n-2) = a^-1 (a != 0): left-to-right sliding 4-bit windows over the
+// constant exponent, odd powers a, a^3, .., a^15 precomputed: 252 squarings +
+// 57 multiplications (the binary method takes 254 + 127).  kInvSched holds
+// (squarings, odd-power index) per window after the first (a^15); generated
+// from n - 2 and checked against pow(a, n - 2, n) by test_host_field_scalar_ops.
 SECP_HD void sc_inv(Sc& r, const Sc& a) {
-  // n - 2, little-endian limbs
-  const u32 e[8] = {0xD036413Fu, 0xBFD25E8Cu, 0xAF48A03Bu, 0xBAAEDCE6u,
-                    0xFFFFFFFEu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-  Sc x = a;
-  // top bit of n-2 is set: start from a
-  for (int bit = 254; bit >= 0; --bit) {
+  constexpr int kWin = 57;
+  constexpr uint8_t kInvSched[2 * kWin] = {4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 4, 7, 3, 3, 5, 5, 3, 2, 4, 2, 4, 3, 5, 6, 2, 1, 5, 3, 6, 6, 5, 5, 4, 6, 3, 0, 6, 2, 10, 3, 4, 3, 5, 7, 4, 7, 5, 4, 6, 5, 4, 6, 5, 1, 6, 6, 10, 6, 4, 4, 9, 4, 4, 7, 1, 0};
+  Sc tbl[8], a2;
+  tbl[0] = a;
+  {
     u32 t[16];
-    sqr_wide(t, x.v);
-    sc_reduce(x, t);
-    if ((e[bit >> 5] >> (bit & 31)) & 1u) sc_mul(x, x, a);
+    sqr_wide(t, a.v);
+    sc_reduce(a2, t);
+  }
+  for (int i = 1; i < 8; ++i) sc_mul(tbl[i], tbl[i - 1], a2);
+  Sc x = tbl[7];
+  for (int k = 0; k < kWin; ++k) {
+    for (int q = 0; q < kInvSched[2 * k]; ++q) {
+      u32 t[16];
+      sqr_wide(t, x.v);
+      sc_reduce(x, t);
+    }
+    sc_mul(x, x, tbl[kInvSched[2 * k + 1]]);
   }
   r = x;
 }
