@@ -11,10 +11,10 @@
 // is_valid_tx at :139); SURVEY §8f row 2.  The per-lane body is
 // dc::secp::check_tx (dc_txsig.h), shared with the host unit test.
 //
-// Cost model: ~3.5k field multiplications per transaction (256 doublings,
-// 64 windowed Jacobian additions, 32 mixed additions from the G table, the
-// s^-1 mod n exponentiation and, for compressed keys, a square root); all
-// integer VALU work (v_mad_u64_u32 chains), no MFMA.
+// Cost model: ~2.7k field multiplications per transaction (GLV: 128 doublings
+// and 66 Jacobian additions for u2 Q, 32 mixed additions from the G table for
+// u1 G, the sliding-window s^-1 mod n and, for compressed keys, a square
+// root); all integer VALU work (Comba v_mad_u64_u32 chains, dc_secp.h), no MFMA.
 #include <hip/hip_runtime.h>
 
 #include "dc_kernels.h"

@@ -57,6 +57,13 @@ extern "C" {
                     root_moves: *mut u16, n_root: *mut u32, total: *mut u64) -> c_int;
     pub fn dc_device_alloc(ctx: *mut dc_ctx, bytes: usize, d_ptr: *mut *mut c_void) -> c_int;
     pub fn dc_device_free(ctx: *mut dc_ctx, d_ptr: *mut c_void) -> c_int;
+    pub fn dc_keccak256(data: *const c_void, len: usize, out: *mut u8) -> c_int;
+    pub fn dc_state_hash(ctx: *mut dc_ctx, start: *const dc_pos, history: *const c_char, names: *const c_char,
+                         names_off: *const u32, moves: *const u16, n_games: u32, n_plies: u32,
+                         hashes: *mut u8) -> c_int;
+    pub fn dc_verify_tx_batch(ctx: *mut dc_ctx, strings: *const c_char, str_off: *const u32, actions: *const u32,
+                              turns: *const i8, n: u32, verdicts: *mut u8) -> c_int;
+    pub fn dc_sig_verdict_message(v: u8) -> *const c_char;
 }
 
 /// One device context (one gfx950 GPU, one HIP stream).  Not Sync: keep one per thread.
