@@ -117,8 +117,14 @@ struct dc_ctx {
   DBuf<DevPos> pos;
   DBuf<uint16_t> moves;
   DBuf<uint8_t> verdicts, info;
-  DBuf<char> hash_text;    // escaped names + start history of dc_state_hash*
-  DBuf<u32> hash_off;
+  DBuf<char> hash_text;    // escaped start history | escaped names of dc_state_hash*
+  DBuf<u32> hash_off;      // the names' escaped offsets into hash_text
+  DBuf<u32> esc_lens;      // device escaping scratch: per-name escaped lengths,
+  DBuf<u64> esc64;         // their scan,
+  DBuf<uint8_t> scan_tmp;  // the scan's temporary storage
+  DBuf<char> names_raw;    // dc_state_hash (host buffers): the raw names staged
+  DBuf<u32> names_raw_off;
+  std::string hist_text;   // the escaped start history (host side of the H2D copy)
   DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
   // transaction-signature check: staged strings / offsets / actions / turns,
@@ -153,6 +159,11 @@ struct dc_ctx {
     info.release();
     hash_text.release();
     hash_off.release();
+    esc_lens.release();
+    esc64.release();
+    scan_tmp.release();
+    names_raw.release();
+    names_raw_off.release();
     hashes.release();
     bitmap.release();
     digests.release();
@@ -625,35 +636,44 @@ u32 count_ws_tokens(const char* s, size_t n) {
   return count;
 }
 
-// Stages the escaped names + start history on the device; returns the
-// history's JSON length and token count.
-int stage_hash_text(dc_ctx* c, const char* history, const char* names, const uint32_t* names_off, uint32_t n_games,
+// Stages the hash kernel's text on the device: hash_text = the start history
+// escaped on the host (one string per batch) followed by the player names
+// escaped on the device from the raw UTF-8 in d_names (serde_json's table,
+// k_escape_len / k_escape_write); hash_off = the names' escaped offsets.  One
+// small readback sizes hash_text from the exact escaped total.
+int stage_hash_text(dc_ctx* c, const char* history, const char* d_names, const uint32_t* d_names_off, uint32_t n_games,
                     u32* hist_len, u32* hist_tokens) {
   const size_t hn = history ? std::strlen(history) : 0;
-  std::string text;
-  text.reserve(hn + (size_t)names_off[(size_t)2 * n_games] + 64);
-  json_escape(history ? history : "", hn, text);
-  *hist_len = (u32)text.size();
+  c->hist_text.clear();
+  json_escape(history ? history : "", hn, c->hist_text);
+  if (c->hist_text.size() > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
+  *hist_len = (u32)c->hist_text.size();
   *hist_tokens = count_ws_tokens(history ? history : "", hn);
-  std::vector<u32> off((size_t)2 * n_games + 1);
-  for (size_t i = 0; i < (size_t)2 * n_games; ++i) {
-    off[i] = (u32)text.size();
-    if (names_off[i + 1] < names_off[i]) return DC_EINVAL;
-    json_escape(names + names_off[i], names_off[i + 1] - names_off[i], text);
-    if (text.size() > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
-  }
-  off[(size_t)2 * n_games] = (u32)text.size();
-  HIP_TRY(c->hash_text.ensure(std::max<size_t>(text.size(), 1)));
-  HIP_TRY(c->hash_off.ensure(off.size()));
-  HIP_TRY(hipMemcpyAsync(c->hash_text.p, text.data(), text.size(), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->hash_off.p, off.data(), off.size() * sizeof(u32), hipMemcpyHostToDevice, c->stream));
-  return sync_ctx(c);  // text / off are host temporaries
+  const u64 n_str = 2ull * n_games;
+  if (n_str + 1 > 0x7FFFFFFFull) return DC_EUNSUPPORTED;  // hipcub's item count is an int
+  const size_t tb = dc::escape_scan_tmp_bytes((u32)n_str);
+  HIP_TRY(c->esc_lens.ensure(n_str + 1));
+  HIP_TRY(c->esc64.ensure(n_str + 1));
+  HIP_TRY(c->scan_tmp.ensure(std::max<size_t>(tb, 1)));
+  HIP_TRY(c->hash_off.ensure(n_str + 1));
+  HIP_TRY(dc::launch_escape_len_scan(c->stream, d_names, d_names_off, (u32)n_str, *hist_len, c->esc_lens.p,
+                                     c->scan_tmp.p, tb, c->esc64.p));
+  u64 total = 0;
+  HIP_TRY(hipMemcpyAsync(&total, c->esc64.p + n_str, sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (total > 0xFFFFFFFFull) return DC_EUNSUPPORTED;  // the hash kernel's offsets are u32
+  HIP_TRY(c->hash_text.ensure(std::max<size_t>(total, 1)));
+  if (*hist_len)
+    HIP_TRY(hipMemcpyAsync(c->hash_text.p, c->hist_text.data(), *hist_len, hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(dc::launch_escape_write(c->stream, d_names, d_names_off, (u32)n_str, c->esc64.p, c->hash_off.p,
+                                  c->hash_text.p));
+  return DC_SUCCESS;
 }
 
-int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const char* names,
-                    const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
+int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const char* d_names,
+                    const uint32_t* d_names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
                     uint8_t* d_hashes) {
-  if (!names || !names_off || (n_games && n_plies && !d_moves) || (n_games && !d_hashes)) return DC_EINVAL;
+  if (!d_names_off || (n_games && n_plies && !d_moves) || (n_games && !d_hashes)) return DC_EINVAL;
   dc_pos s0;
   if (start) s0 = *start;
   else dc_startpos(&s0);
@@ -662,13 +682,13 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
   if (s0.bb[3] & ~(s0.bb[1] | s0.bb[2])) return DC_EUNSUPPORTED;
   if (n_games == 0) return DC_SUCCESS;
   u32 hist_len = 0, hist_tokens = 0;
-  int e = stage_hash_text(c, history, names, names_off, n_games, &hist_len, &hist_tokens);
+  int e = stage_hash_text(c, history, d_names, d_names_off, n_games, &hist_len, &hist_tokens);
   if (e != DC_SUCCESS) return e;
   const Board b{s0.bb[0], s0.bb[1], s0.bb[2], s0.bb[3]};
-  const char* d_names = c->hash_text.p;
+  const char* text = c->hash_text.p;
   HIP_TRY(c->timed("state_hash", n_games, [&] {
-    return dc::launch_state_hash_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, d_names, hist_len, hist_tokens,
-                                     d_names, c->hash_off.p, d_hashes);
+    return dc::launch_state_hash_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, text, hist_len, hist_tokens,
+                                     text, c->hash_off.p, d_hashes);
   }));
   return sync_ctx(c);
 }
@@ -685,11 +705,11 @@ int dc_keccak256(const void* data, size_t len, uint8_t out[32]) {
   return DC_SUCCESS;
 }
 
-int dc_state_hash_device(dc_ctx* c, const dc_pos* start, const char* history, const char* names,
-                         const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
+int dc_state_hash_device(dc_ctx* c, const dc_pos* start, const char* history, const char* d_names,
+                         const uint32_t* d_names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
                          uint8_t* d_hashes) {
   ENTER(c);
-  return state_hash_impl(c, start, history, names, names_off, d_moves, n_games, n_plies, d_hashes);
+  return state_hash_impl(c, start, history, d_names, d_names_off, d_moves, n_games, n_plies, d_hashes);
 }
 
 int dc_state_hash(dc_ctx* c, const dc_pos* start, const char* history, const char* names, const uint32_t* names_off,
@@ -700,7 +720,19 @@ int dc_state_hash(dc_ctx* c, const dc_pos* start, const char* history, const cha
   HIP_TRY(c->moves.ensure(std::max<size_t>(nm, 1)));
   HIP_TRY(c->hashes.ensure(std::max<size_t>((size_t)32 * n_games, 1)));
   if (nm) HIP_TRY(hipMemcpyAsync(c->moves.p, moves, nm * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
-  int r = state_hash_impl(c, start, history, names, names_off, c->moves.p, n_games, n_plies, c->hashes.p);
+  if (n_games) {
+    if (!names || !names_off) return DC_EINVAL;
+    const size_t n_off = (size_t)2 * n_games + 1;
+    for (size_t i = 0; i + 1 < n_off; ++i)
+      if (names_off[i + 1] < names_off[i]) return DC_EINVAL;
+    const size_t raw = names_off[n_off - 1];
+    HIP_TRY(c->names_raw.ensure(std::max<size_t>(raw, 1)));
+    HIP_TRY(c->names_raw_off.ensure(n_off));
+    if (raw) HIP_TRY(hipMemcpyAsync(c->names_raw.p, names, raw, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->names_raw_off.p, names_off, n_off * sizeof(u32), hipMemcpyHostToDevice, c->stream));
+  }
+  int r = state_hash_impl(c, start, history, c->names_raw.p, c->names_raw_off.p, c->moves.p, n_games, n_plies,
+                          c->hashes.p);
   if (r != DC_SUCCESS) return r;
   if (n_games) HIP_TRY(hipMemcpyAsync(hashes, c->hashes.p, (size_t)32 * n_games, hipMemcpyDeviceToHost, c->stream));
   return sync_ctx(c);

@@ -8,4 +8,15 @@ namespace dc {
 hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                                  u32 n_plies, const char* hist, u32 hist_len, u32 hist_tokens, const char* names,
                                  const u32* names_off, uint8_t* out);
+// serde_json escaping of n_str raw UTF-8 strings names[off[i] .. off[i+1]) on
+// the device, in two steps so the host can size the output in between:
+//   len_scan: esc64[i] = base + escaped length of strings 0..i-1 (i <= n_str;
+//             esc64[n_str] = the end); lens[n_str + 1] and tmp
+//             (escape_scan_tmp_bytes) are scratch
+//   write:    out + esc64[i] <- string i escaped; out_off[i] = (u32)esc64[i]
+size_t escape_scan_tmp_bytes(u32 n_str);
+hipError_t launch_escape_len_scan(hipStream_t st, const char* names, const u32* off, u32 n_str, u64 base, u32* lens,
+                                  void* tmp, size_t tmp_bytes, u64* esc64);
+hipError_t launch_escape_write(hipStream_t st, const char* names, const u32* off, u32 n_str, const u64* esc64,
+                               u32* out_off, char* out);
 }  // namespace dc

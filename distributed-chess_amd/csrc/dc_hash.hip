@@ -15,8 +15,10 @@
 // JSON layout (serde_json, struct fields in prost's proto order, game.proto:7-40):
 //   {"turn":T,"white_player":"W","black_player":"B","history":"H",
 //    "board":{"rows":[{"cells":[{"piece":null},{"piece":{"color":0,"kind":"R"}},...]},...]}}
-// Names and the start history arrive JSON-escaped from the host; the tokens
-// the kernel appends are plain ASCII.
+// The start history arrives JSON-escaped from the host (one short string per
+// batch); the player names are escaped on the device (k_escape_len -> scan ->
+// k_escape_write, below) from raw UTF-8 resident in HBM; the tokens the kernel
+// appends are plain ASCII.
 //
 // Per lane: pass 1 replays the game to learn the final turn (the first JSON
 // field); pass 2 replays it again and streams the JSON bytes into the sponge.
@@ -25,6 +27,8 @@
 // board cells); every lane emits exactly one block per step, so the
 // permutations of a wave run together until its lanes' streams end.
 #include <hip/hip_runtime.h>
+
+#include <hipcub/hipcub.hpp>
 
 #include "dc_common.h"
 #include "dc_hash.h"
@@ -282,6 +286,83 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
     o[2] = a[2];
     o[3] = a[3];
   }
+}
+
+// ------------------------------------------------- serde_json name escaping
+// serde_json 1.0's string escape (ser.rs ESCAPE table, the format_escaped_str
+// that serialises GameState's white_player / black_player, game.proto:9-10):
+// '"' and '\\' and \b \t \n \f \r take two bytes, every other byte < 0x20
+// six (\u00xx, lowercase hex), every other byte -- UTF-8 included -- one.
+// One lane per string; names are short, so a lane walks its bytes.
+__device__ __forceinline__ u32 esc_len(u32 ch) {
+  if (ch >= 0x20) return (ch == '"' || ch == '\\') ? 2u : 1u;
+  return (ch == 8 || ch == 9 || ch == 10 || ch == 12 || ch == 13) ? 2u : 6u;
+}
+
+__global__ __launch_bounds__(256) void k_escape_len(const char* __restrict__ names, const u32* __restrict__ off,
+                                                   u32 n_str, u32* __restrict__ lens) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n_str) return;
+  u32 len = 0;
+  if (i < n_str) {
+    const u32 a = off[i], b = off[i + 1];
+    for (u32 k = a; k < b; ++k) len += esc_len((unsigned char)names[k]);  // b < a (malformed): empty
+  }
+  lens[i] = len;  // lens[n_str] = 0: the scan's last entry is the total
+}
+
+// esc64: the exclusive scan of the lengths (u64, so a total past 4 GiB is seen
+// on the host before anything is written); out_off: the same as u32, for the
+// hash kernel.
+__global__ __launch_bounds__(256) void k_escape_write(const char* __restrict__ names, const u32* __restrict__ off,
+                                                     u32 n_str, const u64* __restrict__ esc64,
+                                                     u32* __restrict__ out_off, char* __restrict__ out) {
+  const u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i > n_str) return;
+  out_off[i] = (u32)esc64[i];
+  if (i == n_str) return;
+  const u32 a = off[i], b = off[i + 1];
+  char* o = out + esc64[i];
+  for (u32 k = a; k < b; ++k) {
+    const u32 ch = (unsigned char)names[k];
+    const u32 l = esc_len(ch);
+    if (l == 1) {
+      *o++ = (char)ch;
+    } else if (l == 2) {
+      o[0] = '\\';
+      o[1] = ch == '"' ? '"' : ch == '\\' ? '\\' : ch == 8 ? 'b' : ch == 9 ? 't' : ch == 10 ? 'n' : ch == 12 ? 'f' : 'r';
+      o += 2;
+    } else {
+      o[0] = '\\';
+      o[1] = 'u';
+      o[2] = '0';
+      o[3] = '0';
+      o[4] = (char)('0' + (ch >> 4));
+      const u32 lo = ch & 15;
+      o[5] = (char)(lo < 10 ? '0' + lo : 'a' + lo - 10);
+      o += 6;
+    }
+  }
+}
+
+size_t escape_scan_tmp_bytes(u32 n_str) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceScan::ExclusiveScan(nullptr, bytes, (const u32*)nullptr, (u64*)nullptr, hipcub::Sum(), (u64)0,
+                                          (int)(n_str + 1));
+  return bytes;
+}
+
+hipError_t launch_escape_len_scan(hipStream_t st, const char* names, const u32* off, u32 n_str, u64 base, u32* lens,
+                                  void* tmp, size_t tmp_bytes, u64* esc64) {
+  hipLaunchKernelGGL(k_escape_len, dim3(blocks_for((u64)n_str + 1, 256)), dim3(256), 0, st, names, off, n_str, lens);
+  return hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, lens, esc64, hipcub::Sum(), base, (int)(n_str + 1), st);
+}
+
+hipError_t launch_escape_write(hipStream_t st, const char* names, const u32* off, u32 n_str, const u64* esc64,
+                               u32* out_off, char* out) {
+  hipLaunchKernelGGL(k_escape_write, dim3(blocks_for((u64)n_str + 1, 256)), dim3(256), 0, st, names, off, n_str, esc64,
+                     out_off, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,

@@ -595,8 +595,8 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
 // the other ("special") children go through the LDS slots.
 // PHASE (timing experiments only; wrong counts unless 0): 1 skips the children,
 // 2 also skips the enumeration, leaving the per-parent counts.
-template <int STM, u32 CAP, int PHASE = 0, bool BULK = true>
-__global__ __launch_bounds__(256, 4) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
+template <int STM, u32 CAP, int PHASE = 0, bool BULK = true, int MINW = 4>
+__global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, u64* __restrict__ divide,
                                                  u32* __restrict__ next_chunk) {
   __shared__ C2cShared<CAP> sh;
@@ -869,7 +869,7 @@ static int final_variant() {
   return v;
 }
 
-template <u32 CAP, int PHASE, bool BULK>
+template <u32 CAP, int PHASE, bool BULK, int MINW = 4>
 static void launch_count2c_cap(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
                                u64* divide) {
   // divide is the first member of the run's PerftResult (perft_enqueue): its
@@ -878,10 +878,10 @@ static void launch_count2c_cap(hipStream_t st, int stm, const Board* nodes, cons
   static_assert(offsetof(PerftResult, divide) == 0, "divide heads PerftResult");
   u32* next = &reinterpret_cast<PerftResult*>(divide)->next_chunk;
   if (stm) {
-    auto k = k_count2c<1, CAP, PHASE, BULK>;
+    auto k = k_count2c<1, CAP, PHASE, BULK, MINW>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide, next);
   } else {
-    auto k = k_count2c<0, CAP, PHASE, BULK>;
+    auto k = k_count2c<0, CAP, PHASE, BULK, MINW>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, divide, next);
   }
 }
@@ -893,11 +893,20 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
     const char* e = std::getenv("DC_C2C_PHASE");
     return e ? std::atoi(e) : 0;
   }();
+  // DC_C2C_WAVES (A/B): minimum waves per SIMD of the launch bounds, i.e. the
+  // VGPR budget.  4: 128 VGPRs with 116 B/lane of spills; 3 (default): 156
+  // VGPRs, no scratch.  perft(7) count2 time is the same (0.504 ms), perft(6)
+  // is 10 % faster with 3.
+  static const int waves = [] {
+    const char* e = std::getenv("DC_C2C_WAVES");
+    return e ? std::atoi(e) : 3;
+  }();
   if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
   else if (phase == 7) launch_count2c_cap<256 * 24, 7, true>(st, stm, nodes, tags, rng, divide);
-  else launch_count2c_cap<256 * 24, 0, true>(st, stm, nodes, tags, rng, divide);
+  else if (waves == 4) launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
+  else launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
 }
 
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,

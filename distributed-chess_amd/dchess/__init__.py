@@ -92,8 +92,7 @@ def lib():
                                      C.POINTER(C.c_uint64)]),
         "dc_keccak256": (C.c_int, [_vp, C.c_size_t, _vp]),
         "dc_state_hash": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
-        "dc_state_hash_device": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32,
-                                           _vp]),
+        "dc_state_hash_device": (C.c_int, [_vp, _vp, C.c_char_p, _vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
         "dc_verify_tx_batch": (C.c_int, [_vp, C.c_char_p, _vp, _vp, _vp, C.c_uint32, _vp]),
         "dc_verify_tx_batch_device": (C.c_int, [_vp, _vp, _vp, _vp, _vp, C.c_uint32, _vp]),
         "dc_sig_verdict_message": (C.c_char_p, [C.c_uint8]),
@@ -360,9 +359,23 @@ class Engine:
                                    _ptr(off), _ptr(moves), n_games, n_plies, _ptr(out)), "dc_state_hash")
         return out
 
-    def state_hash_device(self, d_moves, n_games, n_plies, names_blob, names_off, d_hashes, history=""):
-        _check(lib().dc_state_hash_device(self.ctx, None, history.encode(), names_blob, _ptr(names_off), d_moves.ptr,
-                                          n_games, n_plies, d_hashes.ptr), "dc_state_hash_device")
+    def names_device(self, blob, off):
+        """pack_names' (blob, offsets) uploaded once: the resident inputs of
+        state_hash_device.  Returns (d_names, d_names_off)."""
+        d_names = self.alloc(max(len(blob), 1))
+        if blob:
+            d_names.upload(np.frombuffer(blob, np.uint8))
+        d_off = self.alloc(off.nbytes)
+        d_off.upload(np.ascontiguousarray(off, np.uint32))
+        return d_names, d_off
+
+    def state_hash_device(self, d_moves, n_games, n_plies, d_names, d_names_off, d_hashes, history="", start=None):
+        """dc_state_hash_device: every buffer resident on the device (DeviceBuffer);
+        d_names / d_names_off hold pack_names' raw blob and offsets."""
+        sp = np.array([start], POS_DTYPE) if start is not None else None
+        _check(lib().dc_state_hash_device(self.ctx, _ptr(sp) if sp is not None else None, history.encode(),
+                                          d_names.ptr, d_names_off.ptr, d_moves.ptr, n_games, n_plies, d_hashes.ptr),
+               "dc_state_hash_device")
 
     def verify_txs(self, blob, off, actions, turns=None):
         """App::validate_signature (+ the owner check when turns is given) for a

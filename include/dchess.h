@@ -199,13 +199,19 @@ int dc_gen_games_device(dc_ctx* ctx, uint32_t rules, uint64_t seed, uint64_t fir
  * entries.  hashes[32 g .. 32 g + 32) = the 32 digest bytes (alloy B256;
  * "0x" + hex of them is calculate_game_state_hash's String).  A start board
  * holding pieces of unknown kind returns DC_EUNSUPPORTED (their proto kind
- * string is not representable in a dc_pos). */
+ * string is not representable in a dc_pos).
+ *
+ * dc_state_hash_device: the same with d_names, d_names_off, d_moves and
+ * d_hashes in device memory (raw UTF-8, as for dc_state_hash; history stays a
+ * host string).  serde_json's escaping of the names runs on the device; a
+ * decreasing offset pair is taken as an empty name (dc_state_hash rejects it
+ * with DC_EINVAL).  Escaped text past 4 GiB returns DC_EUNSUPPORTED. */
 int dc_keccak256(const void* data, size_t len, uint8_t out[32]);
 int dc_state_hash(dc_ctx* ctx, const dc_pos* start, const char* history, const char* names,
                   const uint32_t* names_off, const uint16_t* moves, uint32_t n_games, uint32_t n_plies,
                   uint8_t* hashes);
-int dc_state_hash_device(dc_ctx* ctx, const dc_pos* start, const char* history, const char* names,
-                         const uint32_t* names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
+int dc_state_hash_device(dc_ctx* ctx, const dc_pos* start, const char* history, const char* d_names,
+                         const uint32_t* d_names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
                          uint8_t* d_hashes);
 
 /* ---------------------------------------------------- transaction signatures

@@ -161,3 +161,51 @@ def test_state_hash_edge_cases(engine):
     cells[0], cells[63] = 5, 8 + 6  # white king, black unknown kind
     with pytest.raises(dchess.DChessError):
         engine.state_hash(np.zeros((2, 1), np.uint16), [("w", "b")], start=dchess.pos_from_cells(cells, 0))
+
+
+@pytest.mark.gpu
+def test_state_hash_device_resident_names(engine):
+    """dc_state_hash_device with moves, raw names and hashes resident on the
+    device: the names are escaped on the GPU (k_escape_len / scan /
+    k_escape_write, serde_json's table).  Every byte 0x00-0x1f, '"', '\\\\',
+    0x7f and multi-byte UTF-8 appear in some name; checked against the oracle
+    and against the host-buffer entry point."""
+    import oracle_lib as O
+    start = O.Pos()
+    n_games, n_plies = 67, 23
+    mv = _games(29, n_games, n_plies, start)
+    ctrl = "".join(chr(c) for c in range(0x20))
+    pool = NAMES + [ctrl, 'x"\\\x7f\b\f\r', "♞" * 40, "a" * 300]
+    names = [(pool[g % len(pool)], pool[(g * 3 + 2) % len(pool)] + str(g)) for g in range(n_games)]
+    blob, off = dchess.pack_names(names)
+    d_names, d_off = engine.names_device(blob, off)
+    d_moves = engine.alloc(mv.nbytes)
+    d_moves.upload(mv)
+    d_h = engine.alloc(32 * n_games)
+    history = "1. e4\x0c"
+    engine.state_hash_device(d_moves, n_games, n_plies, d_names, d_off, d_h, history=history)
+    got = d_h.download(np.uint8, 32 * n_games).reshape(n_games, 32)
+    want = _oracle_hashes(start, history, names, mv)
+    assert (got == want).all()
+    assert (engine.state_hash(mv, names, history=history) == want).all()
+    for b in (d_names, d_off, d_moves, d_h):
+        b.free()
+
+
+@pytest.mark.gpu
+def test_state_hash_rejects_decreasing_offsets(engine):
+    blob, off = dchess.pack_names([("ab", "cd")])
+    off = off.copy()
+    off[1], off[2] = 3, 1
+    mv = np.zeros((1, 1), np.uint16)
+    with pytest.raises(dchess.DChessError):
+        _raw_state_hash(engine, mv, blob, off)
+
+
+def _raw_state_hash(engine, mv, blob, off):
+    import ctypes as C
+    out = np.zeros((mv.shape[1], 32), np.uint8)
+    st = dchess.lib().dc_state_hash(engine.ctx, None, b"", blob, C.c_void_p(off.ctypes.data),
+                                     C.c_void_p(mv.ctypes.data), mv.shape[1], mv.shape[0],
+                                     C.c_void_p(out.ctypes.data))
+    dchess._check(st, "dc_state_hash")

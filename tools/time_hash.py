@@ -14,10 +14,11 @@ d_moves = eng.alloc(n * plies * 2)
 d_h = eng.alloc(n * 32)
 eng.gen_games_device(d_moves, 0x5EED20241022, 0, n, plies, 32)
 blob, off = dchess.pack_names([(f"white{g}", f"black{g}") for g in range(n)])
-eng.state_hash_device(d_moves, n, plies, blob, off, d_h)
+d_names, d_off = eng.names_device(blob, off)
+eng.state_hash_device(d_moves, n, plies, d_names, d_off, d_h)
 eng.set_profiling(True)
 for _ in range(3):
-    eng.state_hash_device(d_moves, n, plies, blob, off, d_h)
+    eng.state_hash_device(d_moves, n, plies, d_names, d_off, d_h)
 eng.set_profiling(False)
 k = eng.kernel_stats("state_hash")
 ms = k["total_ms"] / k["launches"]
