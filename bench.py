@@ -84,7 +84,9 @@ class Dist:
         import torch
         self.torch = torch
         self.dist = None
-        if self.world > 1:
+        # DC_FORCE_DIST=1: the RCCL path at world size 1 (torch.distributed.run
+        # --nproc-per-node 1), to exercise it on a single-GPU box
+        if self.world > 1 or os.environ.get("DC_FORCE_DIST") == "1":
             import torch.distributed as dist
             torch.cuda.set_device(self.local)
             dist.init_process_group("nccl")
@@ -166,24 +168,51 @@ def cpu_baselines(args, threads):
 
 def timed_perft(eng, d, args, pos, depth, steps, warmup):
     """warmup + exactly `steps` timed perft(depth) steps (barrier + device sync on
-    both sides, max over ranks), parity-checked against the golden count."""
+    both sides, max over ranks), parity-checked against the golden count.
+
+    Every timed step is a full perft of this rank's shard, enqueued with
+    dc_perft_repeat_device (the captured launch graph, no host round trip
+    between steps; each step's result stays on the device).  With N > 1 ranks
+    the exchange step -- the all-reduce of each step's per-root-move vector --
+    runs over RCCL on the device, bucketed into one collective after the last
+    step (K x 258 x 8 B instead of K tiny ones); the reduced totals are checked
+    after the timed region."""
     want = REF_STARTPOS.get(depth)
-    for _ in range(warmup):
+    for _ in range(warmup):  # host path: also captures the launch graph for this shard
         tot, _, _ = perft_step(eng, d, args, pos, depth)
         if want is not None and tot != want:
             raise SystemExit(f"parity failure: perft({depth}) = {tot}, expected {want}")
-    # timed region: no per-launch events (they add ~40 us of host work per step)
-    d.sync()
-    t0 = time.perf_counter()
-    leaves = 0
-    for _ in range(steps):
-        tot, _, _ = perft_step(eng, d, args, pos, depth)
-        leaves += tot
-    d.sync()
-    dt = d.max(time.perf_counter() - t0)
-    if want is not None and leaves != want * steps:
-        raise SystemExit(f"parity failure in timed region: {leaves} != {want} x {steps}")
-    return leaves, dt
+    W = 258  # divide[256], n_root | overflow << 32, total
+    if d.dist is None:
+        buf = eng.alloc(steps * W * 8)
+        d.sync()
+        t0 = time.perf_counter()
+        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, buf)
+        eng.synchronize()
+        d.sync()
+        dt = time.perf_counter() - t0
+        res = buf.download(np.uint64, steps * W).reshape(steps, W)
+        buf.free()
+        totals = res[:, 257]
+    else:
+        torch = d.torch
+        t = torch.zeros((steps, W), dtype=torch.int64, device=f"cuda:{d.local}")
+        d.sync()
+        t0 = time.perf_counter()
+        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, t.data_ptr())
+        eng.synchronize()
+        # the exchange step of every timed perft, bucketed: one RCCL all-reduce
+        # (over xGMI) of all steps' per-root-move vectors, n_root words and totals
+        d.dist.all_reduce(t)
+        d.sync()
+        dt = d.max(time.perf_counter() - t0)
+        res = t.cpu().numpy().view(np.uint64)
+        totals = res[:, 257]
+    if (res[:, 256] >> np.uint64(32)).any():
+        raise SystemExit(f"perft({depth}) overflowed its level buffers in the timed region")
+    if want is not None and not (totals == want).all():
+        raise SystemExit(f"parity failure in timed region: {totals.tolist()} != {want}")
+    return int(totals.sum(dtype=np.uint64)), dt
 
 
 def profiled_perft(eng, d, args, pos, depth, steps):

@@ -1101,6 +1101,54 @@ int dc_perft_shard(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth,
   return perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, divide, root_moves, n_root, total);
 }
 
+// n_runs perfts of one position enqueued back to back on the context stream,
+// each run's result left on the device (k_copy_result into d_out + 258 i): no
+// host round trip between runs.  The first call of a configuration runs it once
+// through perft_impl (host sync), which captures the launch sequence; later
+// runs replay that hipGraph.  Returns once the runs are enqueued.
+int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
+                           uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out) {
+  ENTER(c);
+  if (!pos || (n_runs && !d_out) || rules > DC_RULES_FIDE || n_shards == 0 || shard >= n_shards || pos->stm > 1)
+    return DC_EINVAL;
+  if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
+  if (n_runs == 0) return DC_SUCCESS;
+  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
+  const bool graphable = !c->profiling && perft_graphs_enabled();
+  if (!(graphable && c->pgraph && c->pkey == key)) {
+    uint64_t total = 0;
+    int e = perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, nullptr, nullptr, nullptr, &total);
+    if (e != DC_SUCCESS) return e;
+    key.epoch = g_alloc_epoch.load();
+  }
+  const bool use_graph = graphable && c->pgraph && c->pkey == key;
+  const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
+  const uint16_t rm = dc::pack_meta(pos->castle, pos->ep);
+  if (use_graph && (std::memcmp(&c->root_host->b, &rb, sizeof(Board)) != 0 || c->root_host->meta != rm)) {
+    // the graph reads the pinned root block when it runs: runs still queued
+    // (of an earlier position) must finish before it changes
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->root_host->b = rb;
+    c->root_host->meta = rm;
+  }
+  for (u32 i = 0; i < n_runs; ++i) {
+    if (use_graph) {
+      HIP_TRY(hipGraphLaunch(c->pgraph, c->stream));
+    } else {
+      bool host_sync = false;
+      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync);
+      if (e != DC_SUCCESS) return e;
+    }
+    HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, reinterpret_cast<u64*>(d_out) + (size_t)258 * i));
+  }
+  return DC_SUCCESS;
+}
+
+int dc_ctx_synchronize(dc_ctx* c) {
+  ENTER(c);
+  return sync_ctx(c);
+}
+
 // One process, several GPUs: a host thread per device computes its shard of
 // the frontier, then one grouped ncclAllReduce(ncclUint64, ncclSum) over the
 // per-device divide[] vectors combines them over xGMI.

@@ -41,6 +41,9 @@ hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* n
                               const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
                               const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap);
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
+// out[0..256) = the run's divide (0 past n_root), out[256] = n_root | overflow << 32,
+// out[257] = the total: one run's result kept on the device (dc_perft_repeat_device).
+hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, u64* out);
 // Strided shard: every n_shards-th node of the level, gathered to out[0..).
 hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* in_meta, const uint16_t* in_tags,
                                Range* rng, u32 shard, u32 n_shards, Board* out, uint16_t* out_meta,

@@ -854,6 +854,25 @@ hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* 
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void k_copy_result(const PerftResult* __restrict__ r, u64* __restrict__ out) {
+  __shared__ u64 ws[4];
+  const u32 i = threadIdx.x, nr = r->n_root;
+  const u64 v = i < nr ? r->divide[i] : 0;
+  out[i] = v;
+  const u64 s = wave_sum64(v);
+  if (lane_id() == 0) ws[i >> 6] = s;
+  __syncthreads();
+  if (i == 0) {
+    out[256] = (u64)nr | ((u64)r->overflow << 32);
+    out[257] = ws[0] + ws[1] + ws[2] + ws[3];
+  }
+}
+
+hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, u64* out) {
+  hipLaunchKernelGGL(k_copy_result, dim3(1), dim3(256), 0, st, res, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
   hipLaunchKernelGGL(k_slice, dim3(1), dim3(1), 0, st, rng, shard, n_shards);
   return hipGetLastError();

@@ -88,6 +88,9 @@ def lib():
                                C.POINTER(C.c_uint64)]),
         "dc_perft_shard": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, _vp,
                                      _vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+        "dc_perft_repeat_device": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, _vp]),
+        "dc_ctx_synchronize": (C.c_int, [_vp]),
         "dc_multi_perft": (C.c_int, [_vp, C.c_int, C.c_uint32, _vp, C.c_uint32, _vp, _vp, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint64)]),
         "dc_keccak256": (C.c_int, [_vp, C.c_size_t, _vp]),
@@ -423,6 +426,23 @@ class Engine:
         _check(lib().dc_perft_shard(self.ctx, rules, _ptr(p), depth, split_depth, shard, n_shards, _ptr(div),
                                     _ptr(rm), C.byref(nr), C.byref(tot)), "dc_perft_shard")
         return int(tot.value), div[:nr.value].copy(), rm[:nr.value].copy()
+
+    def perft_repeat_device(self, pos, depth, split_depth, shard, n_shards, n_runs, d_out, rules=RULES_REF):
+        """dc_perft_repeat_device: n_runs perfts enqueued back to back, run i's
+        result at device address d_out + 8 * 258 * i (divide[256], n_root |
+        overflow << 32, total); d_out is a DeviceBuffer or a raw device address.
+        Returns once enqueued (see synchronize)."""
+        p = np.array([pos], POS_DTYPE)
+        ptr = d_out.ptr if hasattr(d_out, "ptr") else _vp(int(d_out))
+        _check(lib().dc_perft_repeat_device(self.ctx, rules, _ptr(p), depth, split_depth, shard, n_shards, n_runs,
+                                            ptr), "dc_perft_repeat_device")
+
+    def synchronize(self):
+        _check(lib().dc_ctx_synchronize(self.ctx), "dc_ctx_synchronize")
+
+    def stream(self):
+        """The context's hipStream_t as an int (for torch.cuda.ExternalStream)."""
+        return int(lib().dc_ctx_stream(self.ctx) or 0)
 
 
 def multi_perft(devices, pos, depth, rules=RULES_REF):

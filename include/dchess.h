@@ -259,6 +259,21 @@ int dc_perft_shard(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t dept
                    uint32_t shard, uint32_t n_shards, uint64_t* divide, uint16_t* root_moves,
                    uint32_t* n_root, uint64_t* total);
 
+/* n_runs perfts of *pos (depth >= 2; shard as dc_perft_shard) enqueued back to
+ * back on the context stream with no host round trip between them.  Run i
+ * leaves its result in DEVICE memory d_out[258 i .. 258 i + 258):
+ *   [0, 256) divide per root move (0 past n_root; root-move order as dc_perft)
+ *   [256]    n_root | overflow << 32  (overflow != 0: redo with dc_perft_shard)
+ *   [257]    total leaves of this shard
+ * Returns once the runs are enqueued; dc_ctx_synchronize (or an event on
+ * dc_ctx_stream) orders the caller after them.  For throughput work (a suite
+ * of repeated perfts, the bench's timed steps, a device-side all-reduce of
+ * each run's divide vector). */
+int dc_perft_repeat_device(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
+                           uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out);
+/* Blocks until all work queued on the context stream has finished. */
+int dc_ctx_synchronize(dc_ctx* ctx);
+
 /* ------------------------------------------------------------- multi-GPU
  * One process, n_devices GPUs, one RCCL communicator (ncclCommInitAll); the
  * frontier is sharded contiguously and divide[] is combined with

@@ -342,6 +342,36 @@ def test_perft_shards_sum(engine, n_shards, split):
     assert t == tot and (acc == div).all()
 
 
+@pytest.mark.parametrize("depth,n_shards", [(5, 1), (6, 1), (6, 3), (3, 2)])
+def test_perft_repeat_device(engine, depth, n_shards):
+    """dc_perft_repeat_device: runs enqueued back to back (graph replays), each
+    run's divide / n_root / total left on the device, equal to dc_perft_shard."""
+    s = dchess.startpos()
+    runs = 3
+    W = 258
+    for k in range(n_shards):
+        st, sd, srm = engine.perft_shard(s, depth, 3 if depth >= 5 else 1, k, n_shards)
+        buf = engine.alloc(runs * W * 8)
+        engine.perft_repeat_device(s, depth, 3 if depth >= 5 else 1, k, n_shards, runs, buf)
+        engine.synchronize()
+        res = buf.download(np.uint64, runs * W).reshape(runs, W)
+        buf.free()
+        for r in res:
+            assert int(r[256]) == len(srm)  # n_root, no overflow
+            assert int(r[257]) == st
+            assert (r[:len(srm)] == sd).all() and not r[len(srm):256].any()
+    # a different position after queued runs of the first (the pinned root block changes)
+    mid = dchess.pos_from_fen("rnbqkbnr/pppp1ppp/8/4p3/4P3/8/PPPP1PPP/RNBQKBNR w - - 0 2")
+    want, _, _ = engine.perft(mid, 4)
+    buf = engine.alloc(2 * W * 8)
+    engine.perft_repeat_device(s, 4, 1, 0, 1, 1, buf)
+    engine.perft_repeat_device(mid, 4, 1, 0, 1, 1, int(buf.ptr.value) + W * 8)
+    engine.synchronize()
+    res = buf.download(np.uint64, 2 * W).reshape(2, W)
+    buf.free()
+    assert int(res[0, 257]) == 197742 and int(res[1, 257]) == want
+
+
 def test_multi_perft_single_device_rccl():
     """dc_multi_perft over one device: RCCL communicator + all-reduce path."""
     s = dchess.startpos()
