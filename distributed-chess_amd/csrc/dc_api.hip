@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -109,6 +110,10 @@ struct dc_ctx {
     }
   } pkey{};
   hipGraphExec_t pgraph = nullptr;
+  // dc_perft_repeat_device's graph: the same sequence without the root upload
+  // and the result readback (the root stays on the device between runs)
+  hipGraphExec_t rgraph = nullptr;
+  PerftKey rkey{};
   struct RootStage {
     Board b;
     uint16_t meta;
@@ -152,6 +157,7 @@ struct dc_ctx {
     rng.release();
     desc.release();
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
+    if (rgraph) (void)hipGraphExecDestroy(rgraph);
     if (res_host) (void)hipHostFree(res_host);
     if (root_host) (void)hipHostFree(root_host);
     pos.release();
@@ -220,6 +226,8 @@ struct dc_ctx {
   } while (0)
 
 static int map_hip_error(hipError_t e) {
+  static const bool debug = std::getenv("DC_DEBUG") != nullptr;
+  if (debug) std::fprintf(stderr, "dchess: HIP error %d (%s)\n", (int)e, hipGetErrorString(e));
   if (e == hipErrorOutOfMemory) return DC_ENOMEM;
   if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) return DC_ENODEV;
   if (e == hipErrorNotSupported) return DC_EUNSUPPORTED;
@@ -837,7 +845,7 @@ int dc_gen_games(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first_game, 
 namespace {
 
 constexpr u64 kBranchBound = 64;                    // speculative children per node
-constexpr u64 kSpecBudget = 4ull << 30;             // bytes per speculative level
+constexpr u64 kSpecBudget = 16ull << 30;            // bytes per speculative level (of 288 GB HBM)
 constexpr u64 kNodeBytes = sizeof(Board) + 2 * sizeof(uint16_t);
 
 int ensure_level(dc_ctx* c, int b, u64 n, bool fide) {
@@ -870,7 +878,7 @@ static bool shard_contiguous() {
 // (exact mode or a level beyond the speculative budget): such a sequence
 // depends on data and is never captured as a graph.
 int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
-                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync) {
+                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true) {
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   const u32 F = depth >= 3 ? depth - 2 : 1;       // level handed to the final stage
@@ -900,11 +908,13 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     ts.meta[k] = fide ? c->top_meta.p + off : nullptr;
     ts.cap[k] = kTopCap[k + 1];
   }
-  // root upload from pinned memory, result block cleared
-  c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
-  c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
-  HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  // root upload from pinned memory (stage_root = false: the caller staged it), result block cleared
+  if (stage_root) {
+    c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
+    c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
+    HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  }
   HIP_TRY(hipMemsetAsync(c->res.p, 0, sizeof(dc::PerftResult), c->stream));
   HIP_TRY(c->timed("expand_top", 0, [&] {
     return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, ts, c->nodes[0].p,
@@ -949,13 +959,19 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   };
   while (L < F) {
     const int stm = pos->stm ^ (L & 1);
-    if (exact || nb * kBranchBound * kNodeBytes > kSpecBudget) {
+    if (exact) {
       *host_sync = true;
       e = read_range(c, L, &nb);
       if (e != DC_SUCCESS) return e;
     }
-    u64 cap_next = nb * kBranchBound;
-    const bool exact_next = exact || cap_next * kNodeBytes > kSpecBudget;
+    // Speculative mode never reads a level size back: the next level gets
+    // min(64 x bound, kSpecBudget) of capacity, a level past it is dropped and
+    // flagged (k_chunk_scan) and the run redone in exact mode.  The level
+    // kernels use resident grids over device Ranges, so a loose bound costs
+    // memory, not launches.  (Reading the ply-4 size back cost perft(7) one
+    // host sync mid-run and kept it out of the graph.)
+    u64 cap_next = exact ? nb * kBranchBound : std::min(nb * kBranchBound, kSpecBudget / kNodeBytes);
+    const bool exact_next = exact;
     e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0);
     if (e != DC_SUCCESS) return e;
     if (exact_next) {
@@ -1115,25 +1131,49 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
   if (n_runs == 0) return DC_SUCCESS;
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
   const bool graphable = !c->profiling && perft_graphs_enabled();
-  if (!(graphable && c->pgraph && c->pkey == key)) {
+  if (!c->root_host || !(graphable && c->rgraph && c->rkey == key)) {
+    // a plain run (host sync) sizes the buffers and stages the root; then the
+    // sequence is captured without the root upload and the readback
     uint64_t total = 0;
     int e = perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, nullptr, nullptr, nullptr, &total);
     if (e != DC_SUCCESS) return e;
     key.epoch = g_alloc_epoch.load();
+    if (graphable) {
+      if (c->rgraph) {
+        (void)hipGraphExecDestroy(c->rgraph);
+        c->rgraph = nullptr;
+      }
+      if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+        bool hs = false;
+        const int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
+        hipGraph_t g = nullptr;
+        const hipError_t ee = hipStreamEndCapture(c->stream, &g);
+        if (ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
+            hipGraphInstantiate(&c->rgraph, g, nullptr, nullptr, 0) == hipSuccess)
+          c->rkey = key;
+        else
+          c->rgraph = nullptr;
+        if (g) (void)hipGraphDestroy(g);
+      }
+      (void)hipGetLastError();
+    }
   }
-  const bool use_graph = graphable && c->pgraph && c->pkey == key;
+  const bool use_graph = graphable && c->rgraph && c->rkey == key;
   const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
   const uint16_t rm = dc::pack_meta(pos->castle, pos->ep);
   if (use_graph && (std::memcmp(&c->root_host->b, &rb, sizeof(Board)) != 0 || c->root_host->meta != rm)) {
-    // the graph reads the pinned root block when it runs: runs still queued
-    // (of an earlier position) must finish before it changes
+    // every staging copies root_host to the device root, so the device root
+    // holds *pos once queued work is done if root_host does; else restage
+    // (after the runs still queued have read the pinned block)
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->root_host->b = rb;
     c->root_host->meta = rm;
+    HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
   for (u32 i = 0; i < n_runs; ++i) {
     if (use_graph) {
-      HIP_TRY(hipGraphLaunch(c->pgraph, c->stream));
+      HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));
     } else {
       bool host_sync = false;
       int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync);
