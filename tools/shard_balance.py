@@ -12,6 +12,7 @@ import dchess  # noqa: E402
 depth = int(sys.argv[1]) if len(sys.argv) > 1 else 7
 e = dchess.Engine(0)
 s = dchess.startpos()
+e.perft(s, depth)  # first touch of the level buffers (16 GB speculative caps) outside the timings
 for split in [int(x) for x in os.environ.get("SPLITS", "3 4").split()]:
     for R in (2, 4, 8):
         rows = []
