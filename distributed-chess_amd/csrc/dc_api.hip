@@ -476,6 +476,15 @@ uint16_t dc_move_pack(uint32_t fx, uint32_t fy, uint32_t tx, uint32_t ty) {
   return (uint16_t)((8 * fx + fy) | ((8 * tx + ty) << 6));
 }
 
+int dc_move_pack_batch(const uint32_t* actions, uint32_t n, uint16_t* moves) {
+  if (n && (!actions || !moves)) return DC_EINVAL;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t* a = actions + (size_t)4 * i;
+    moves[i] = dc_move_pack(a[0], a[1], a[2], a[3]);
+  }
+  return DC_SUCCESS;
+}
+
 // ============================================================== validation
 int dc_validate_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, const uint16_t* moves, uint32_t n,
                       uint8_t* verdicts) {

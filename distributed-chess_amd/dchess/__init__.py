@@ -75,6 +75,7 @@ def lib():
         "dc_pos_to_cells": (C.c_int, [_vp, _vp, C.POINTER(C.c_uint8)]),
         "dc_pos_from_fen": (C.c_int, [C.c_char_p, _vp]),
         "dc_move_pack": (C.c_uint16, [C.c_uint32] * 4),
+        "dc_move_pack_batch": (C.c_int, [_vp, C.c_uint32, _vp]),
         "dc_validate_batch": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, _vp]),
         "dc_apply_batch": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, _vp, _vp]),
         "dc_replay": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, C.POINTER(_Stats)]),
@@ -236,6 +237,15 @@ def pos_from_fen(fen):
 
 def move_pack(fx, fy, tx, ty):
     return int(lib().dc_move_pack(fx, fy, tx, ty))
+
+
+def move_pack_batch(actions):
+    """uint32 actions [n, 4] (from.x, from.y, to.x, to.y per transaction) ->
+    uint16 move words (dc_move_pack_batch)."""
+    actions = np.ascontiguousarray(actions, np.uint32).reshape(-1, 4)
+    out = np.zeros(len(actions), np.uint16)
+    _check(lib().dc_move_pack_batch(_ptr(actions), len(actions), _ptr(out)), "dc_move_pack_batch")
+    return out
 
 
 class DeviceBuffer:

@@ -148,6 +148,12 @@ int dc_pos_to_cells(const dc_pos* pos, int8_t cells[64], uint8_t* turn);
 int dc_pos_from_fen(const char* fen, dc_pos* out);
 /* Position{x,y} pair -> move word; any coordinate >= 8 sets DC_MOVE_OOR. */
 uint16_t dc_move_pack(uint32_t from_x, uint32_t from_y, uint32_t to_x, uint32_t to_y);
+/* A block's Transaction.action lists (core/proto/query.proto:46-49, the u32
+ * Position pairs of is_valid_tx's action[0..2], hotstuff.rs:138) -> move words:
+ * actions[4i .. 4i+4) = from.x, from.y, to.x, to.y (the dc_verify_tx_batch
+ * layout, so one packed block feeds both checks); moves[i] = dc_move_pack of
+ * them, DC_MOVE_OOR for any coordinate >= 8 (where the reference panics). */
+int dc_move_pack_batch(const uint32_t* actions, uint32_t n, uint16_t* moves);
 
 /* ------------------------------------------------------------- validation
  * verdicts[i] = verdict of moves[i] in pos[i] (rules per call). */

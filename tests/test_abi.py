@@ -86,6 +86,23 @@ def test_fen_parser_matches_oracle():
         dchess.pos_from_fen("not a fen")
 
 
+def test_move_pack_batch():
+    """Transaction.action u32 coordinates (query.proto:46-49) -> move words: in range
+    packs f | t << 6, any coordinate >= 8 (up to 2^32 - 1) is DC_MOVE_OOR."""
+    rng = np.random.default_rng(7)
+    a = rng.integers(0, 8, (500, 4), dtype=np.uint32)
+    big = rng.integers(8, 2**32, (500, 4), dtype=np.uint64).astype(np.uint32)
+    pick = rng.random((500, 4)) < 0.1
+    a = np.where(pick, big, a)
+    got = dchess.move_pack_batch(a)
+    want = [dchess.move_pack(*map(int, r)) for r in a]
+    assert got.tolist() == want
+    ok = ~pick.any(axis=1)
+    assert (got[ok] == (a[ok, 0] * 8 + a[ok, 1]) | ((a[ok, 2] * 8 + a[ok, 3]) << 6)).all()
+    assert (got[~ok] == dchess.MOVE_OOR).all()
+    assert dchess.move_pack_batch(np.zeros((0, 4), np.uint32)).size == 0
+
+
 def test_move_pack():
     assert dchess.move_pack(1, 0, 3, 0) == (8 | (24 << 6))
     assert dchess.move_pack(8, 0, 0, 0) == dchess.MOVE_OOR
