@@ -917,14 +917,14 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     ts.meta[k] = fide ? c->top_meta.p + off : nullptr;
     ts.cap[k] = kTopCap[k + 1];
   }
-  // root upload from pinned memory (stage_root = false: the caller staged it), result block cleared
+  // root upload from pinned memory (stage_root = false: the caller staged it)
   if (stage_root) {
     c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
     c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
     HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
-  HIP_TRY(hipMemsetAsync(c->res.p, 0, sizeof(dc::PerftResult), c->stream));
+  // the result block is cleared by k_expand_top itself (its first stores)
   HIP_TRY(c->timed("expand_top", 0, [&] {
     return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, ts, c->nodes[0].p,
                                  fide ? c->meta[0].p : nullptr, c->tags[0].p, cap_T, c->res.p, c->rng.p + T);

@@ -157,6 +157,10 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
   __shared__ uint16_t s_root_tag;
   __shared__ Board s_root;
   __shared__ uint16_t s_root_meta;
+  // the run's result block is cleared here, not by a separate memset launch
+  // (one ~5 us graph node less per perft)
+  static_assert(sizeof(PerftResult) % 8 == 0, "PerftResult is cleared in u64 words");
+  for (u32 k = threadIdx.x; k < sizeof(PerftResult) / 8; k += kTopThreads) reinterpret_cast<u64*>(res)[k] = 0;
   if (threadIdx.x == 0) {
     s_root_tag = 0;
     s_root = root[0];
