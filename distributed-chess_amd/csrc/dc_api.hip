@@ -114,6 +114,9 @@ struct dc_ctx {
   // and the result readback (the root stays on the device between runs)
   hipGraphExec_t rgraph = nullptr;
   PerftKey rkey{};
+  // the last perft_impl needed the exact (host-sized) rerun: its speculative
+  // level capacities overflow, so dc_perft_repeat_device must not replay them
+  bool last_exact = false;
   struct RootStage {
     Board b;
     uint16_t meta;
@@ -876,10 +879,28 @@ int read_range(dc_ctx* c, int level, u64* n) {
 
 static bool shard_contiguous() {
   static const bool v = [] {
-    const char* e = std::getenv("DC_SHARD");
+    const char* e = dc::ab_env("DC_SHARD");
     return e && std::strcmp(e, "contig") == 0;
   }();
   return v;
+}
+
+// Writes *pos into the pinned root staging block.  Copies already queued on
+// the stream (dc_perft_repeat_device returns with runs in flight, each reading
+// the block when it executes) must see the value they were queued with, so a
+// changed root first waits for the stream.  A capture only ever re-stages the
+// root of the run that was just synchronised (the value is unchanged).
+int write_root_host(dc_ctx* c, const dc_pos* pos) {
+  const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
+  const uint16_t rm = dc::pack_meta(pos->castle, pos->ep);
+  if (std::memcmp(&c->root_host->b, &rb, sizeof(Board)) == 0 && c->root_host->meta == rm) return DC_SUCCESS;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIP_TRY(hipStreamIsCapturing(c->stream, &cs));
+  if (cs != hipStreamCaptureStatusNone) return DC_EHIP;  // unreachable: captures follow a synchronised run
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->root_host->b = rb;
+  c->root_host->meta = rm;
+  return DC_SUCCESS;
 }
 
 // Enqueues one perft on the context stream up to (not including) the result
@@ -919,8 +940,8 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   }
   // root upload from pinned memory (stage_root = false: the caller staged it)
   if (stage_root) {
-    c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
-    c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
+    e = write_root_host(c, pos);
+    if (e != DC_SUCCESS) return e;
     HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
@@ -1018,7 +1039,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
 // DC_GRAPH=0 disables the perft graph (A/B).
 static bool perft_graphs_enabled() {
   static const bool on = [] {
-    const char* e = std::getenv("DC_GRAPH");
+    const char* e = dc::ab_env("DC_GRAPH");
     return !(e && e[0] == '0');
   }();
   return on;
@@ -1034,10 +1055,10 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
   const bool graphable = !exact && !c->profiling && perft_graphs_enabled();
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
   if (graphable && c->pgraph && c->pkey == key) {
-    c->root_host->b = Board{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
-    c->root_host->meta = dc::pack_meta(pos->castle, pos->ep);
+    int e = write_root_host(c, pos);
+    if (e != DC_SUCCESS) return e;
     HIP_TRY(hipGraphLaunch(c->pgraph, c->stream));
-    int e = sync_ctx(c);
+    e = sync_ctx(c);
     if (e != DC_SUCCESS) return e;
     *out = *c->res_host;
     return DC_SUCCESS;
@@ -1090,7 +1111,8 @@ int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uin
   }
   dc::PerftResult r;
   int e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r);
-  if (e == DC_SUCCESS && r.overflow) e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, true, &r);
+  c->last_exact = e == DC_SUCCESS && r.overflow;
+  if (c->last_exact) e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, true, &r);
   if (e != DC_SUCCESS) return e;
   if (r.overflow) return DC_EUNSUPPORTED;  // more than 256 root moves, or a level beyond 2^32 nodes
   const u32 nr = r.n_root;
@@ -1146,6 +1168,17 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     uint64_t total = 0;
     int e = perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, nullptr, nullptr, nullptr, &total);
     if (e != DC_SUCCESS) return e;
+    if (c->last_exact) {
+      // speculative capacities overflow for this configuration: exact runs
+      // (one host sync per level), each result still left on the device
+      for (u32 i = 0; i < n_runs; ++i) {
+        bool hs = false;
+        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs);
+        if (e != DC_SUCCESS) return e;
+        HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, reinterpret_cast<u64*>(d_out) + (size_t)258 * i));
+      }
+      return DC_SUCCESS;
+    }
     key.epoch = g_alloc_epoch.load();
     if (graphable) {
       if (c->rgraph) {
@@ -1173,10 +1206,9 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
   if (use_graph && (std::memcmp(&c->root_host->b, &rb, sizeof(Board)) != 0 || c->root_host->meta != rm)) {
     // every staging copies root_host to the device root, so the device root
     // holds *pos once queued work is done if root_host does; else restage
-    // (after the runs still queued have read the pinned block)
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    c->root_host->b = rb;
-    c->root_host->meta = rm;
+    // (write_root_host waits for the runs still queued to read the pinned block)
+    int e = write_root_host(c, pos);
+    if (e != DC_SUCCESS) return e;
     HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
@@ -1229,16 +1261,20 @@ int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_p
   for (int r : rc)
     if (r != DC_SUCCESS) result = r;
   std::vector<u64> div(256, 0);
+  // every shard rebuilds the same root moves: a disagreement is a bug, never summed over
+  for (int i = 1; i < n_devices && result == DC_SUCCESS; ++i)
+    if (nroot[i] != nroot[0]) result = DC_EHIP;
   if (result == DC_SUCCESS && depth > 0) {
     std::vector<ncclComm_t> comms(n_devices);
     if (ncclCommInitAll(comms.data(), n_devices, devices) != ncclSuccess) {
       result = DC_ERCCL;
     } else {
-      ncclGroupStart();
-      for (int i = 0; i < n_devices; ++i) {
-        (void)hipSetDevice(devices[i]);
-        ncclAllReduce(ctx[i]->res.p->divide, ctx[i]->res.p->divide, nroot[0], ncclUint64, ncclSum, comms[i],
-                      ctx[i]->stream);
+      if (ncclGroupStart() != ncclSuccess) result = DC_ERCCL;
+      for (int i = 0; i < n_devices && result == DC_SUCCESS; ++i) {
+        if (hipSetDevice(devices[i]) != hipSuccess) result = DC_EHIP;
+        else if (ncclAllReduce(ctx[i]->res.p->divide, ctx[i]->res.p->divide, nroot[0], ncclUint64, ncclSum, comms[i],
+                               ctx[i]->stream) != ncclSuccess)
+          result = DC_ERCCL;
       }
       if (ncclGroupEnd() != ncclSuccess) result = DC_ERCCL;
       for (int i = 0; i < n_devices; ++i) {
@@ -1273,4 +1309,129 @@ int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_p
   return result;
 }
 
+
+// ---------------------------------------------------------- multi-GPU replay
+// Contiguous game-id ranges of whole 64-game bitmap words, so shard s's accept
+// bitmap [n_plies][count/64] is a word-column block of the global ply-major
+// bitmap [n_plies][ceil(n_games/64)], at word offset first/64.
+int dc_replay_shard_range(uint64_t n_games, uint32_t shard, uint32_t n_shards, uint64_t* first, uint64_t* count) {
+  if (!first || !count || n_shards == 0 || shard >= n_shards) return DC_EINVAL;
+  const u64 words = (n_games + 63) / 64, per = (words + n_shards - 1) / n_shards;
+  const u64 lo = std::min<u64>(n_games, std::min<u64>(words, (u64)shard * per) * 64);
+  const u64 hi = std::min<u64>(n_games, std::min<u64>(words, (u64)(shard + 1) * per) * 64);
+  *first = lo;
+  *count = hi > lo ? hi - lo : 0;
+  return DC_SUCCESS;
+}
+
+// One process, n_devices GPUs: device i generates (dc_gen_games_device) and
+// replays (dc_replay_device) shard i of the game ids; the per-shard bitmaps
+// go to device 0 with one ncclGather over xGMI (rccl.h:745) and from there to
+// the host; the five counters are folded on the host (sums mod 2^64, xor).
+int dc_multi_replay(const int* devices, int n_devices, uint32_t rules, uint64_t seed, uint64_t n_games,
+                    uint32_t n_plies, uint32_t noise_per_256, uint64_t* bitmap, dc_replay_stats* stats) {
+  if (!devices || n_devices <= 0 || rules > DC_RULES_FIDE || noise_per_256 > 256) return DC_EINVAL;
+  const u64 words = (n_games + 63) / 64, per = (words + n_devices - 1) / n_devices;
+  if (per * 64 > 0xFFFFFFFFull) return DC_EUNSUPPORTED;  // a shard's game count is a u32
+  std::vector<dc_ctx*> ctx(n_devices, nullptr);
+  for (int i = 0; i < n_devices; ++i) {
+    int r = dc_ctx_create(devices[i], &ctx[i]);
+    if (r != DC_SUCCESS) {
+      for (auto* x : ctx)
+        if (x) dc_ctx_destroy(x);
+      return r;
+    }
+  }
+  const size_t shard_words = (size_t)per * n_plies;  // every shard's bitmap padded to `per` words per ply
+  std::vector<int> rc(n_devices, DC_SUCCESS);
+  std::vector<dc_replay_stats> st(n_devices);
+  std::vector<void*> d_moves(n_devices, nullptr), d_bm(n_devices, nullptr);
+  void* d_all = nullptr;  // device 0: the gathered [n_devices][n_plies][per]
+  std::vector<std::thread> th;
+  for (int i = 0; i < n_devices; ++i)
+    th.emplace_back([&, i] {
+      uint64_t first = 0, cnt = 0;
+      int r = dc_replay_shard_range(n_games, (u32)i, (u32)n_devices, &first, &cnt);
+      if (r == DC_SUCCESS) r = dc_device_alloc(ctx[i], std::max<size_t>((size_t)cnt * n_plies * 2, 2), &d_moves[i]);
+      if (r == DC_SUCCESS) r = dc_device_alloc(ctx[i], std::max<size_t>(shard_words * 8, 8), &d_bm[i]);
+      if (r == DC_SUCCESS && i == 0 && bitmap)
+        r = dc_device_alloc(ctx[i], std::max<size_t>(shard_words * 8 * n_devices, 8), &d_all);
+      if (r == DC_SUCCESS && hipMemsetAsync(d_bm[i], 0, shard_words * 8, ctx[i]->stream) != hipSuccess) r = DC_EHIP;
+      if (r == DC_SUCCESS)
+        r = dc_gen_games_device(ctx[i], rules, seed, first, (u32)cnt, n_plies, noise_per_256,
+                                static_cast<uint16_t*>(d_moves[i]));
+      // the shard's bitmap rows are `per` words apart: replay into a dense
+      // [n_plies][cnt/64] block, then spread the rows (dense = padded when full)
+      if (r == DC_SUCCESS) {
+        const u64 w_r = (cnt + 63) / 64;
+        void* dense = d_bm[i];
+        if (w_r != per && cnt) r = dc_device_alloc(ctx[i], (size_t)w_r * n_plies * 8, &dense);
+        if (r == DC_SUCCESS)
+          r = dc_replay_device(ctx[i], rules, nullptr, static_cast<uint16_t*>(d_moves[i]), (u32)cnt, n_plies,
+                               static_cast<uint64_t*>(dense), nullptr, &st[i]);
+        if (r == DC_SUCCESS && dense != d_bm[i]) {
+          if (hipMemcpy2DAsync(d_bm[i], per * 8, dense, w_r * 8, w_r * 8, n_plies, hipMemcpyDeviceToDevice,
+                               ctx[i]->stream) != hipSuccess)
+            r = DC_EHIP;
+          else
+            r = sync_ctx(ctx[i]);
+          dc_device_free(ctx[i], dense);
+        }
+      }
+      rc[i] = r;
+    });
+  for (auto& t : th) t.join();
+  int result = DC_SUCCESS;
+  for (int r : rc)
+    if (r != DC_SUCCESS) result = r;
+  if (result == DC_SUCCESS && bitmap && n_plies && words) {
+    std::vector<ncclComm_t> comms(n_devices);
+    if (ncclCommInitAll(comms.data(), n_devices, devices) != ncclSuccess) {
+      result = DC_ERCCL;
+    } else {
+      if (ncclGroupStart() != ncclSuccess) result = DC_ERCCL;
+      for (int i = 0; i < n_devices && result == DC_SUCCESS; ++i) {
+        if (hipSetDevice(devices[i]) != hipSuccess) result = DC_EHIP;
+        else if (ncclGather(d_bm[i], i == 0 ? d_all : nullptr, shard_words, ncclUint64, 0, comms[i], ctx[i]->stream) !=
+                 ncclSuccess)
+          result = DC_ERCCL;
+      }
+      if (ncclGroupEnd() != ncclSuccess) result = DC_ERCCL;
+      for (int i = 0; i < n_devices; ++i) {
+        (void)hipSetDevice(devices[i]);
+        if (hipStreamSynchronize(ctx[i]->stream) != hipSuccess) result = DC_EHIP;
+      }
+      for (auto& cm : comms) ncclCommDestroy(cm);
+    }
+    // device 0 -> host: shard i's rows land at word offset first_i / 64 of each ply row
+    for (int i = 0; i < n_devices && result == DC_SUCCESS; ++i) {
+      uint64_t first = 0, cnt = 0;
+      dc_replay_shard_range(n_games, (u32)i, (u32)n_devices, &first, &cnt);
+      const u64 w_r = (cnt + 63) / 64;
+      if (!w_r) continue;
+      (void)hipSetDevice(devices[0]);
+      if (hipMemcpy2D(bitmap + first / 64, words * 8, static_cast<const u64*>(d_all) + (size_t)i * shard_words,
+                      per * 8, w_r * 8, n_plies, hipMemcpyDeviceToHost) != hipSuccess)
+        result = DC_EHIP;
+    }
+  }
+  if (result == DC_SUCCESS && stats) {
+    dc_replay_stats t{0, 0, 0, 0, 0};
+    for (auto& x : st) {
+      t.validated += x.validated;
+      t.accepted += x.accepted;
+      t.rejected += x.rejected;
+      t.digest_sum += x.digest_sum;
+      t.digest_xor ^= x.digest_xor;
+    }
+    *stats = t;
+  }
+  for (int i = 0; i < n_devices; ++i) {
+    if (d_moves[i]) dc_device_free(ctx[i], d_moves[i]);
+    if (d_bm[i]) dc_device_free(ctx[i], d_bm[i]);
+  }
+  if (d_all) dc_device_free(ctx[0], d_all);
+  for (auto* x : ctx) dc_ctx_destroy(x);
+  return result;
+}
 }  // extern "C"

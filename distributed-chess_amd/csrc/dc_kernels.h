@@ -2,8 +2,22 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace dc {
+
+// A/B knobs (kernel-variant and timing experiments) are compiled only into
+// the A/B build (`make ab` -> libdchess_ab.so, -DDC_AB_KNOBS): the shipped
+// libdchess.so reads no environment variable that selects a kernel or
+// changes a result, so a replica's environment cannot alter its verdicts.
+inline const char* ab_env(const char* name) {
+#ifdef DC_AB_KNOBS
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 typedef unsigned long long u64;
 typedef uint32_t u32;

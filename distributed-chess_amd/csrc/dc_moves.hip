@@ -546,7 +546,7 @@ u32 replay_partials(u32 n_games) { return blocks_for(n_games, 256); }
 // validate kernels) instead of the LDS-table k_replay_ref3, for A/B and parity.
 static bool replay_arith() {
   static const bool v = [] {
-    const char* e = std::getenv("DC_REPLAY");
+    const char* e = ab_env("DC_REPLAY");
     return e && e[0] == '1';
   }();
   return v;

@@ -598,7 +598,8 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
 // counted per parent as n_simple x (base + pawn_O) and never enumerated; only
 // the other ("special") children go through the LDS slots.
 // PHASE (timing experiments only; wrong counts unless 0): 1 skips the children,
-// 2 also skips the enumeration, leaving the per-parent counts.
+// 2 also skips the enumeration, leaving the per-parent counts.  Phases other
+// than 0 are instantiated only in the A/B build (-DDC_AB_KNOBS, libdchess_ab.so).
 template <int STM, u32 CAP, int PHASE = 0, bool BULK = true, int MINW = 4>
 __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, u64* __restrict__ divide,
@@ -886,7 +887,7 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
 // under REF (k_count2c: 24 child slots per parent, the best of 20/24/28).
 static int final_variant() {
   static const int v = [] {
-    const char* e = std::getenv("DC_FINAL");
+    const char* e = ab_env("DC_FINAL");
     return (e && std::strcmp(e, "2b") == 0) ? 0 : 1;
   }();
   return v;
@@ -913,7 +914,7 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
                            u64* divide) {
   // DC_C2C_PHASE (A/B and timing only): 3 = no bulk split; 1, 2 = partial phases
   static const int phase = [] {
-    const char* e = std::getenv("DC_C2C_PHASE");
+    const char* e = ab_env("DC_C2C_PHASE");
     return e ? std::atoi(e) : 0;
   }();
   // DC_C2C_WAVES (A/B): minimum waves per SIMD of the launch bounds, i.e. the
@@ -921,15 +922,21 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
   // VGPRs, no scratch.  perft(7) count2 time is the same (0.504 ms), perft(6)
   // is 10 % faster with 3.
   static const int waves = [] {
-    const char* e = std::getenv("DC_C2C_WAVES");
+    const char* e = ab_env("DC_C2C_WAVES");
     return e ? std::atoi(e) : 3;
   }();
+#ifdef DC_AB_KNOBS
   if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
   else if (phase == 7) launch_count2c_cap<256 * 24, 7, true>(st, stm, nodes, tags, rng, divide);
   else if (waves == 4) launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
   else launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
+#else
+  (void)phase;
+  (void)waves;
+  launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
+#endif
 }
 
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,

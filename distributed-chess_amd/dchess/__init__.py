@@ -14,7 +14,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(PKG_DIR), "libdchess.so")
+# DCHESS_LIB selects another build of the same ABI -- only tools/ab_*.sh use it,
+# for libdchess_ab.so (the A/B-knob build, `make ab`).
+LIB_PATH = os.environ.get("DCHESS_LIB") or os.path.join(os.path.dirname(PKG_DIR), "libdchess.so")
 
 SUCCESS, EINVAL, EHIP, ENOMEM, ENODEV, ERCCL, EUNSUPPORTED = 0, -1, -2, -3, -4, -5, -6
 V_OK, V_NO_PIECE, V_WRONG_TURN, V_ILLEGAL, V_OOR = 0, 1, 2, 3, 4
@@ -94,6 +96,10 @@ def lib():
         "dc_ctx_synchronize": (C.c_int, [_vp]),
         "dc_multi_perft": (C.c_int, [_vp, C.c_int, C.c_uint32, _vp, C.c_uint32, _vp, _vp, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint64)]),
+        "dc_replay_shard_range": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
+                                            C.POINTER(C.c_uint64)]),
+        "dc_multi_replay": (C.c_int, [_vp, C.c_int, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
+                                      _vp, C.POINTER(_Stats)]),
         "dc_keccak256": (C.c_int, [_vp, C.c_size_t, _vp]),
         "dc_state_hash": (C.c_int, [_vp, _vp, C.c_char_p, C.c_char_p, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
         "dc_state_hash_device": (C.c_int, [_vp, _vp, C.c_char_p, _vp, _vp, _vp, C.c_uint32, C.c_uint32, _vp]),
@@ -123,6 +129,13 @@ def _check(status, what):
 
 def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def _dptr(d):
+    """A DeviceBuffer, a raw device address (int) or None -> c_void_p."""
+    if d is None:
+        return None
+    return d.ptr if hasattr(d, "ptr") else _vp(int(d))
 
 
 def verdict_message(v):
@@ -352,10 +365,11 @@ class Engine:
         return bitmap, dig, {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
 
     def replay_device(self, d_moves, n_games, n_plies, d_bitmap=None, d_digests=None, rules=RULES_REF):
+        """d_* are DeviceBuffers or raw device addresses (e.g. a torch tensor's
+        data_ptr(), for buffers that a torch.distributed collective reads)."""
         st = _Stats()
-        _check(lib().dc_replay_device(self.ctx, rules, None, d_moves.ptr, n_games, n_plies,
-                                      d_bitmap.ptr if d_bitmap else None, d_digests.ptr if d_digests else None,
-                                      C.byref(st)), "dc_replay_device")
+        _check(lib().dc_replay_device(self.ctx, rules, None, _dptr(d_moves), n_games, n_plies, _dptr(d_bitmap),
+                                      _dptr(d_digests), C.byref(st)), "dc_replay_device")
         return {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
 
     def state_hash(self, moves, names, start=None, history=""):
@@ -415,7 +429,7 @@ class Engine:
 
     def gen_games_device(self, d_out, seed, first_game, n_games, n_plies, noise_per_256=32, rules=RULES_REF):
         _check(lib().dc_gen_games_device(self.ctx, rules, seed, first_game, n_games, n_plies, noise_per_256,
-                                         d_out.ptr), "dc_gen_games_device")
+                                         _dptr(d_out)), "dc_gen_games_device")
 
     # --------------------------------------------------------------- perft
     def perft(self, pos, depth, rules=RULES_REF):
@@ -464,6 +478,26 @@ def multi_perft(devices, pos, depth, rules=RULES_REF):
     _check(lib().dc_multi_perft(devs, len(devices), rules, _ptr(p), depth, _ptr(div), _ptr(rm), C.byref(nr),
                                 C.byref(tot)), "dc_multi_perft")
     return int(tot.value), div[:nr.value].copy(), rm[:nr.value].copy()
+
+
+def replay_shard_range(n_games, shard, n_shards):
+    """(first game id, count) of one replay shard (dc_replay_shard_range)."""
+    first, count = C.c_uint64(), C.c_uint64()
+    _check(lib().dc_replay_shard_range(int(n_games), int(shard), int(n_shards), C.byref(first), C.byref(count)),
+           "dc_replay_shard_range")
+    return int(first.value), int(count.value)
+
+
+def multi_replay(devices, seed, n_games, n_plies, noise_per_256=32, rules=RULES_REF, want_bitmap=True):
+    """dc_multi_replay: the seeded games [0, n_games) over several devices of this
+    process.  Returns (bitmap [n_plies][ceil(n_games/64)] or None, stats dict)."""
+    devs = (C.c_int * len(devices))(*devices)
+    words = (n_games + 63) // 64
+    bitmap = np.zeros((n_plies, words), np.uint64) if want_bitmap else None
+    st = _Stats()
+    _check(lib().dc_multi_replay(devs, len(devices), rules, seed, n_games, n_plies, noise_per_256, _ptr(bitmap),
+                                 C.byref(st)), "dc_multi_replay")
+    return bitmap, {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
 
 
 # ---------------------------------------------------------------------------

@@ -258,9 +258,11 @@ const char* dc_sig_verdict_message(uint8_t verdict);
 int dc_perft(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint64_t* divide,
              uint16_t* root_moves, uint32_t* n_root, uint64_t* total);
 /* One shard of perft for data-parallel runs: the frontier at ply `split_depth`
- * is built deterministically, and this call counts only frontier nodes
- * [shard*N/n_shards, (shard+1)*N/n_shards).  Summing divide[] over all shards
- * (e.g. an RCCL all-reduce) gives dc_perft's result exactly. */
+ * (N nodes) is built deterministically, and this call counts only the subtrees
+ * of the STRIDED shard of it -- frontier nodes shard, shard + n_shards,
+ * shard + 2*n_shards, ... < N (k_gather_shard; strided shards hold equal leaf
+ * counts to about 1 %, contiguous ones did not).  Summing divide[] over all
+ * shards (e.g. an RCCL all-reduce) gives dc_perft's result exactly. */
 int dc_perft_shard(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
                    uint32_t shard, uint32_t n_shards, uint64_t* divide, uint16_t* root_moves,
                    uint32_t* n_root, uint64_t* total);
@@ -281,11 +283,29 @@ int dc_perft_repeat_device(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint3
 int dc_ctx_synchronize(dc_ctx* ctx);
 
 /* ------------------------------------------------------------- multi-GPU
- * One process, n_devices GPUs, one RCCL communicator (ncclCommInitAll); the
- * frontier is sharded contiguously and divide[] is combined with
- * ncclAllReduce(ncclUint64, ncclSum) over xGMI. */
+ * One process, n_devices GPUs, one RCCL communicator (ncclCommInitAll); device
+ * i counts strided shard i of the frontier (dc_perft_shard) and divide[] is
+ * combined with ncclAllReduce(ncclUint64, ncclSum) over xGMI. */
 int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_pos* pos, uint32_t depth,
                    uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total);
+
+/* Replay shard contract: game ids [0, n_games) are split into
+ * contiguous ranges of whole 64-game bitmap words -- with W = ceil(n_games/64)
+ * words and P = ceil(W/n_shards), shard s holds games [min(n_games, min(W, sP)*64),
+ * min(n_games, min(W, (s+1)P)*64)) -- so its ply-major accept bitmap is the
+ * word-column block [first/64, first/64 + ceil(count/64)) of every ply row of
+ * the whole batch's bitmap.  Data-parallel callers (one process per GPU)
+ * replay their own range and combine: validated / accepted / rejected /
+ * digest_sum add (mod 2^64), digest_xor xors, bitmaps are gathered. */
+int dc_replay_shard_range(uint64_t n_games, uint32_t shard, uint32_t n_shards, uint64_t* first, uint64_t* count);
+/* The seeded games [0, n_games) (dc_gen_games' generator: seed, n_plies,
+ * noise_per_256) generated and replayed on n_devices GPUs of one process,
+ * shard i on device i.  bitmap (optional, HOST) = the whole batch's ply-major
+ * [n_plies][ceil(n_games/64)] accept bitmap: the shards' bitmaps are gathered
+ * to devices[0] with ncclGather over xGMI, then copied out; stats = the
+ * combined counters. */
+int dc_multi_replay(const int* devices, int n_devices, uint32_t rules, uint64_t seed, uint64_t n_games,
+                    uint32_t n_plies, uint32_t noise_per_256, uint64_t* bitmap, dc_replay_stats* stats);
 
 #ifdef __cplusplus
 }

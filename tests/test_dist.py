@@ -1,8 +1,15 @@
-"""Multi-process (world_size 2, gloo on CPU) tests of the data-parallel perft
-combine in dchess/dist.py.  The per-rank shard is computed by a CPU stand-in
-built on the oracle (test double only): frontier at ply `split` in the
-oracle's canonical order, contiguous slice, subtree perft per root move --
-the same shard contract as dc_perft_shard."""
+"""Multi-process (world_size 2, gloo on CPU) tests of the data-parallel
+combines in dchess/dist.py.
+
+Perft: the per-rank shard is computed by a CPU stand-in built on the oracle
+(test double only): frontier at ply `split` in the oracle's canonical order,
+the STRIDED shard of it (nodes rank, rank + world, ...), subtree perft per
+root move -- the shard contract of dc_perft_shard.
+
+Replay: each rank generates and replays its dc_replay_shard_range range with
+the oracle (the stand-in for dc_gen_games_device + dc_replay_device), then
+dist.combine_replay folds the counters and gathers the bitmaps to rank 0,
+which must equal one replay of the whole batch."""
 import os
 import socket
 
@@ -20,10 +27,8 @@ def oracle_shard(pos_fen, depth, split, shard, n_shards, rules=O.REF):
     frontier = [(i, O.fast_make(root, int(m), rules)) for i, m in enumerate(roots)]
     for _ in range(split - 1):
         frontier = [(i, O.fast_make(p, int(m), rules)) for i, p in frontier for m in O.fast_gen_moves(p, rules)]
-    n = len(frontier)
-    lo, hi = n * shard // n_shards, n * (shard + 1) // n_shards
     div = np.zeros(len(roots), np.uint64)
-    for i, p in frontier[lo:hi]:
+    for i, p in frontier[shard::n_shards]:
         div[i] += O.fast_perft(p, depth - split, rules, threads=1)[0]
     return int(div.sum()), div, roots
 
@@ -78,6 +83,71 @@ def test_two_rank_gloo_perft(case):
     for _, tot, div, rm in res:
         assert tot == want
         assert dict(zip(rm, div)) == dict(zip(wrm.tolist(), wdiv.tolist()))
+
+
+def _replay_worker(rank, world, port, n_total, q):
+    import sys
+    sys.path[:0] = PATHS
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import torch
+    import dchess.dist as D
+    first, count = D.replay_range(n_total, rank, world)
+    mv = O.fast_gen_games(SEED, first, count, 24, 32, threads=1)
+    bm, _, st = O.fast_replay(mv, threads=1)
+    stats, whole = D.combine_replay(st, torch.from_numpy(bm.view(np.int64)), n_total, rank, world)
+    q.put((rank, stats, None if whole is None else whole.tolist()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+SEED = 0x5EED20241022
+
+
+@pytest.mark.parametrize("n_total", [1000, 64 * 7])
+def test_two_rank_gloo_replay_combine(n_total):
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_replay_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=90) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    mv = O.fast_gen_games(SEED, 0, n_total, 24, 32, threads=1)
+    bm, _, st = O.fast_replay(mv, threads=1)
+    want = dict(zip(("validated", "accepted", "rejected", "digest_sum", "digest_xor"), (int(x) for x in st)))
+    for rank, stats, whole in res:
+        assert stats == want
+        if rank == 0:
+            assert (np.array(whole, np.uint64) == bm).all()
+        else:
+            assert whole is None
+
+
+def test_replay_range_matches_abi():
+    """dist.replay_range is the contract of dc_replay_shard_range (host-only call)."""
+    import dchess
+    import dchess.dist as D
+    for n in (0, 1, 63, 64, 65, 1000, 10_000_000, 100_000_000):
+        for world in (1, 2, 3, 4, 8):
+            seen = 0
+            for r in range(world):
+                got = dchess.replay_shard_range(n, r, world)
+                assert got == D.replay_range(n, r, world)
+                first, count = got
+                assert first == seen and (first % 64 == 0 or first == n)
+                seen += count
+            assert seen == n
+
+
+def test_fold_stats_wraps_mod_2_64():
+    import dchess.dist as D
+    big = (1 << 64) - 5
+    got = D.fold_stats([[1, 1, 0, big, 3], [2, 1, 1, 10, 5]])
+    assert got == {"validated": 3, "accepted": 2, "rejected": 1, "digest_sum": 5, "digest_xor": 6}
 
 
 def test_game_ranges_partition():

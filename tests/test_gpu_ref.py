@@ -372,6 +372,28 @@ def test_perft_repeat_device(engine, depth, n_shards):
     assert int(res[0, 257]) == 197742 and int(res[1, 257]) == want
 
 
+def test_perft_repeat_device_profiling_then_other_position(engine):
+    """With profiling on, dc_perft_repeat_device enqueues plain (non-graph) runs,
+    each copying the pinned root block when it executes; a perft of another
+    position issued right after must not overwrite that block under them."""
+    s = dchess.startpos()
+    mid = dchess.pos_from_fen("rnbqkbnr/pppp1ppp/8/4p3/4P3/8/PPPP1PPP/RNBQKBNR w - - 0 2")
+    want_mid, _, _ = engine.perft(mid, 5)
+    W, runs = 258, 4
+    buf = engine.alloc(runs * W * 8)
+    engine.set_profiling(True)
+    try:
+        engine.perft_repeat_device(s, 5, 3, 0, 1, runs, buf)
+        got_mid, _, _ = engine.perft(mid, 5)  # host path: writes the pinned root block
+        engine.synchronize()
+    finally:
+        engine.set_profiling(False)
+    res = buf.download(np.uint64, runs * W).reshape(runs, W)
+    buf.free()
+    assert got_mid == want_mid
+    assert (res[:, 257] == 4896998).all()
+
+
 def test_multi_perft_single_device_rccl():
     """dc_multi_perft over one device: RCCL communicator + all-reduce path."""
     s = dchess.startpos()

@@ -2,6 +2,9 @@
 # A/B of the REF final stage (k_count2b vs k_count2c at several slot caps):
 # parity tests first, then perft(7)/perft(6) bench lines per variant.
 export TMPDIR=/tmp
+# the knobs below exist only in the A/B build (make -C distributed-chess_amd ab)
+export DCHESS_LIB=$PWD/distributed-chess_amd/libdchess_ab.so
+[ -f "$DCHESS_LIB" ] || { echo "build libdchess_ab.so first (make -C distributed-chess_amd ab)"; exit 3; }
 O=gpurun_out; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "perft or replica" > $O/ab_pytest.log 2>&1 || { tail -30 $O/ab_pytest.log; exit 1; }
 tail -2 $O/ab_pytest.log

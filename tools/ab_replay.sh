@@ -2,6 +2,9 @@
 # A/B of the REF replay kernel (DC_REPLAY=1: arithmetic k_replay_ref; default:
 # LDS-table k_replay_ref2): replay parity tests, then replay bench lines.
 export TMPDIR=/tmp
+# the knobs below exist only in the A/B build (make -C distributed-chess_amd ab)
+export DCHESS_LIB=$PWD/distributed-chess_amd/libdchess_ab.so
+[ -f "$DCHESS_LIB" ] || { echo "build libdchess_ab.so first (make -C distributed-chess_amd ab)"; exit 3; }
 O=gpurun_out; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "replay or gen or apply or validate or smoke" > $O/abr_pytest.log 2>&1 || { tail -30 $O/abr_pytest.log; exit 1; }
 tail -2 $O/abr_pytest.log
