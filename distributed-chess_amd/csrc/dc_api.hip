@@ -97,6 +97,7 @@ struct dc_ctx {
   DBuf<dc::PerftResult> res;
   DBuf<dc::Range> rng;
   DBuf<u64> desc;
+  DBuf<u64> dfs_stack;  // K4 frames (dc_perft.hip k_perft_dfs)
   DBuf<Board> root;
   DBuf<uint16_t> root_meta;
   dc::PerftResult* res_host = nullptr;  // pinned
@@ -117,6 +118,7 @@ struct dc_ctx {
   // the last perft_impl needed the exact (host-sized) rerun: its speculative
   // level capacities overflow, so dc_perft_repeat_device must not replay them
   bool last_exact = false;
+  const char* last_final = "count2";  // timing name of the last perft's final stage
   struct RootStage {
     Board b;
     uint16_t meta;
@@ -159,6 +161,7 @@ struct dc_ctx {
     res.release();
     rng.release();
     desc.release();
+    dfs_stack.release();
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (rgraph) (void)hipGraphExecDestroy(rgraph);
     if (res_host) (void)hipHostFree(res_host);
@@ -859,6 +862,10 @@ namespace {
 constexpr u64 kBranchBound = 64;                    // speculative children per node
 constexpr u64 kSpecBudget = 16ull << 30;            // bytes per speculative level (of 288 GB HBM)
 constexpr u64 kNodeBytes = sizeof(Board) + 2 * sizeof(uint16_t);
+// Deepest BFS level under REF: below it, K4 (k_perft_dfs) walks per lane.
+// Ply 5 of startpos is 4.9M nodes (196 MB); a typical middlegame ply 5 stays
+// within the speculative budget (Kiwipete's is 193M nodes, 6.6 GB).
+constexpr u32 kDfsFrontier = 5;
 
 int ensure_level(dc_ctx* c, int b, u64 n, bool fide) {
   const size_t want = std::max<u64>(n, 1);
@@ -911,7 +918,15 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
                   uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true) {
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
-  const u32 F = depth >= 3 ? depth - 2 : 1;       // level handed to the final stage
+  u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
+  // REF beyond ply kDfsFrontier: K4 walks the last Ldfs plies above the final
+  // stage per lane (k_perft_dfs) instead of materialising those levels
+  u32 Ldfs = 0;
+  if (!fide && depth >= 3 && F > kDfsFrontier) {
+    Ldfs = F - kDfsFrontier;
+    F = kDfsFrontier;
+    if (Ldfs > 3) return DC_EUNSUPPORTED;
+  }
   const int final_plies = depth >= 3 ? 2 : 1;     // depth 1: no final stage
   const u32 S = std::max<u32>(1, std::min(split_depth, F));
   u32 T = exact ? 1 : std::min<u32>(F, 3);        // plies built by the single-workgroup top kernel
@@ -1027,7 +1042,15 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     }
   }
   const int stm = pos->stm ^ (L & 1);
-  if (depth >= 2) {
+  c->last_final = Ldfs > 0 ? "dfs" : final_plies == 2 ? "count2" : "count1";
+  if (Ldfs > 0) {
+    const u64 lanes = dc::dfs_lanes();
+    if (Ldfs > 1) HIP_TRY(c->dfs_stack.ensure((size_t)(Ldfs - 1) * 7 * lanes));
+    HIP_TRY(c->timed("dfs", 0, [&] {
+      return dc::launch_perft_dfs(c->stream, stm ^ (int)(Ldfs & 1), Ldfs, c->nodes[buf].p, c->tags[buf].p,
+                                  c->rng.p + L, c->res.p, Ldfs > 1 ? c->dfs_stack.p : nullptr, lanes);
+    }));
+  } else if (depth >= 2) {
     HIP_TRY(c->timed(final_plies == 2 ? "count2" : "count1", 0, [&] {
       return dc::launch_final(c->stream, rules, stm, final_plies, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
                               c->tags[buf].p, c->rng.p + L, nb, c->res.p->divide, nullptr);
@@ -1126,7 +1149,7 @@ int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uin
   }
   *total = t;
   if (c->profiling && depth >= 2) {
-    auto it = c->stats.find(depth >= 3 ? "count2" : "count1");
+    auto it = c->stats.find(c->last_final);  // the final stage that ran
     if (it != c->stats.end()) it->second.units += t;
   }
   return DC_SUCCESS;

@@ -18,6 +18,8 @@ struct PerftResult {
   u32 path;        // final stage: 0 descriptor list, 1 LDS count2
   u32 next_chunk;  // k_count2c's dynamic chunk counter (zeroed with the block)
   u64 level_n[16];
+  u32 dfs_next;    // k_perft_dfs's frontier cursor (zeroed with the block)
+  u32 pad0;
 };
 
 // Scratch of the single-workgroup top expansion (plies 1 and 2).
@@ -53,5 +55,13 @@ hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* 
 // when res->path == 1).
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
                         const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res);
+
+// K4 (REF): per-lane DFS over L plies below the frontier level `rng` (1 <= L <= 3),
+// each level-L node bulk-counted over the last two plies (perft depth = frontier
+// ply + L + 2).  stm_parent = side to move at the level-L nodes.  stack_frames
+// holds (L - 1) x 7 x lanes u64 (null for L == 1); lanes = dfs_lanes().
+u64 dfs_lanes();
+hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* nodes, const uint16_t* tags,
+                            const Range* rng, PerftResult* res, u64* stack_frames, u64 lanes);
 
 }  // namespace dc

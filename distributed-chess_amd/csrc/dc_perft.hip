@@ -600,14 +600,159 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
 // PHASE (timing experiments only; wrong counts unless 0): 1 skips the children,
 // 2 also skips the enumeration, leaving the per-parent counts.  Phases other
 // than 0 are instantiated only in the A/B build (-DDC_AB_KNOBS, libdchess_ab.so).
+// One group of 256 parents (one per thread; `valid` false for an empty slot):
+// the last two plies below each, added into the block's divide histogram.
+// Called by k_count2c (parents read from a level in HBM) and k_perft_dfs
+// (parents produced by each lane's DFS stack).  Block-uniform call; ends with
+// a block barrier (par/att/ptag/slot are reused by the next group).
+template <int STM, u32 CAP, int PHASE = 0, bool BULK = true>
+__device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const Board& p, u32 tag,
+                                          u64* __restrict__ divide) {
+  const u32 tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+  u32* q = sh.queue[w];
+  u32 cnt = 0, base = 0;
+  u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
+  u32 nsim = 0;
+  if (valid) {
+    if constexpr (BULK) {
+      ParentSplit ps;
+      ref_parent_split<STM>(p, ps);
+      base = ps.base;
+      att = ps.att;
+      Fs = ps.Fs;
+      Ts = ps.Ts;
+      cnt = ps.n_total - ps.n_simple;  // enumerated (special) children only
+      simple_leaves = (u64)ps.n_simple * (ps.base + ps.pawn_o);
+      nsim = ps.n_simple;
+    } else {
+      cnt = ref_count<STM>(p);
+      base = ref_count_nonpawn<1 - STM>(p, att);
+    }
+  }
+  u64 total64;
+  const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
+  const u32 total = (u32)total64;
+  sh.par[tid] = p;
+  sh.att[tid] = att;
+  sh.base[tid] = base;
+  sh.ptag[tid] = (uint16_t)tag;
+  __syncthreads();
+  const u32 tag0 = sh.ptag[0];
+  u64 acc = 0;  // grandchildren under parents whose tag == tag0
+  auto add = [&](u32 pl, u32 k, bool live) {
+    if constexpr (PHASE == 7) return;
+    if (!live) return;
+    const u32 ptag = sh.ptag[pl];
+    if (ptag == tag0) acc += k;
+    else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
+  };
+  u32 qn = 0;  // queue length: wave-uniform (kept scalar via readfirstlane)
+  // One candidate child: its parent's LDS record is loaded first (so two
+  // candidates' loads can be in flight together), then the short path if the
+  // move is quiet, else the child is appended to the queue.
+  struct Cand {
+    u32 e, base;
+    Board pb;
+    u64 a;
+  };
+  auto fetch = [&](u32 e) {
+    const u32 pl = e >> 15;
+    return Cand{e, sh.base[pl], sh.par[pl], sh.att[pl]};
+  };
+  auto consume = [&](const Cand& c, bool live) {
+    const u32 pl = c.e >> 15;
+    const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
+    const u64 occ = occupied(c.pb);
+    const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
+    if (live && quiet) add(pl, c.base + ref_pawn_count_child<1 - STM>(c.pb, f, t), true);
+    const bool full = live && !quiet;
+    const u64 em = ballot(full);
+    if constexpr (PHASE == 7) {  // statistics: divide[0] quiet special children, [1] full-recount children
+      const u64 qm = ballot(live && quiet);
+      if (lane == 0) {
+        atomicAdd((unsigned long long*)divide, (unsigned long long)__popcll(qm));
+        atomicAdd((unsigned long long*)(divide + 1), (unsigned long long)__popcll(em));
+      }
+    }
+    if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
+    qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
+  };
+  auto drain64 = [&]() {  // qn >= 64: recount 64 queued children in full
+    wave_lds_sync();
+    const u32 e2 = q[lane];
+    add(e2 >> 15, c2c_full<STM>(sh, e2), true);
+    wave_lds_sync();
+    if (lane + 64 < qn) q[lane] = q[lane + 64];
+    qn = __builtin_amdgcn_readfirstlane(qn - 64);
+  };
+  if constexpr (BULK && PHASE != 7) add(tid, (u32)simple_leaves, valid);
+  if constexpr (PHASE == 7) {  // [2] simple children, [3] parents
+    const u64 ns = wave_sum64(nsim), np = __popcll(ballot(valid));
+    if (lane == 0) {
+      atomicAdd((unsigned long long*)(divide + 2), (unsigned long long)ns);
+      atomicAdd((unsigned long long*)(divide + 3), (unsigned long long)np);
+    }
+  }
+  if constexpr (PHASE == 1 || PHASE == 2) acc += cnt + base + (u32)att;
+  for (u32 wbase = 0; wbase < (PHASE == 2 ? 0u : total); wbase += CAP) {
+    if (wbase) __syncthreads();  // previous window fully read
+    // each (f, t) of this parent's enumerated (BULK: special) moves -> visit(f, t)
+    auto each_move = [&](auto&& visit) {
+      if constexpr (BULK) ref_for_each_special<STM>(p, Fs, Ts, visit);
+      else ref_for_each_move<STM>(p, visit);
+    };
+    if (total <= CAP) {  // the norm: one window, no range checks
+      u32 j = excl;
+      if (valid) each_move([&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | (tid << 15); });
+    } else {
+      u32 j = excl;
+      if (valid && j < wbase + CAP && j + cnt > wbase) {
+        each_move([&](int f, int t) {
+          if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
+          ++j;
+        });
+      }
+    }
+    __syncthreads();
+    const u32 nslots = min(CAP, total - wbase);
+    // two slots per lane per step, loaded together, so the LDS round trips overlap
+    u32 r0 = (PHASE == 1 || PHASE == 2) ? nslots : w * 64;
+    for (; r0 + 256 < nslots; r0 += 512) {
+      const u32 ra = r0 + lane, rb = r0 + 256 + lane;
+      const bool lb = rb < nslots;
+      const Cand ca = fetch(sh.slot[ra]);
+      const Cand cb = fetch(lb ? sh.slot[rb] : 0u);
+      consume(ca, true);
+      if (qn >= 64) drain64();
+      consume(cb, lb);
+      if (qn >= 64) drain64();
+    }
+    if (r0 < nslots) {
+      const u32 ra = r0 + lane;
+      const bool la = ra < nslots;
+      consume(fetch(la ? sh.slot[ra] : 0u), la);
+      if (qn >= 64) drain64();
+    }
+  }
+  // drain this wave's queue (par/att of the chunk are still in LDS)
+  if (qn) {
+    wave_lds_sync();
+    const bool live = lane < qn;
+    const u32 e2 = live ? q[lane] : 0u;
+    const u32 k = live ? c2c_full<STM>(sh, e2) : 0u;
+    add(e2 >> 15, k, live);
+  }
+  tag_hist_add(sh.hist, tag0, acc, true);
+  __syncthreads();  // par/att/ptag/slot reused by the next group
+}
+
 template <int STM, u32 CAP, int PHASE = 0, bool BULK = true, int MINW = 4>
 __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, u64* __restrict__ divide,
                                                  u32* __restrict__ next_chunk) {
   __shared__ C2cShared<CAP> sh;
   tag_hist_init(sh.hist);
-  const u32 tid = threadIdx.x, w = tid >> 6, lane = lane_id();
-  u32* q = sh.queue[w];
+  const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
   // Blocks take 256-parent chunks from a counter: the cost of a chunk varies
   // with its positions, and static ranges left the slowest block behind (a
@@ -620,142 +765,119 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
     const u64 i = s + tid;
     const bool valid = i < hi;
     Board p{0, 0, 0, 0};
-    u32 tag = 0, cnt = 0, base = 0;
-    u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
-    u32 nsim = 0;
+    u32 tag = 0;
     if (valid) {
       p = load_board(nodes, i);
       tag = tags[i];
-      if constexpr (BULK) {
-        ParentSplit ps;
-        ref_parent_split<STM>(p, ps);
-        base = ps.base;
-        att = ps.att;
-        Fs = ps.Fs;
-        Ts = ps.Ts;
-        cnt = ps.n_total - ps.n_simple;  // enumerated (special) children only
-        simple_leaves = (u64)ps.n_simple * (ps.base + ps.pawn_o);
-        nsim = ps.n_simple;
-      } else {
-        cnt = ref_count<STM>(p);
-        base = ref_count_nonpawn<1 - STM>(p, att);
-      }
     }
-    u64 total64;
-    const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
-    const u32 total = (u32)total64;
-    sh.par[tid] = p;
-    sh.att[tid] = att;
-    sh.base[tid] = base;
-    sh.ptag[tid] = (uint16_t)tag;
-    __syncthreads();
-    const u32 tag0 = sh.ptag[0];
-    u64 acc = 0;  // grandchildren under parents whose tag == tag0
-    auto add = [&](u32 pl, u32 k, bool live) {
-      if constexpr (PHASE == 7) return;
-      if (!live) return;
-      const u32 ptag = sh.ptag[pl];
-      if (ptag == tag0) acc += k;
-      else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
-    };
-    u32 qn = 0;  // queue length: wave-uniform (kept scalar via readfirstlane)
-    // One candidate child: its parent's LDS record is loaded first (so two
-    // candidates' loads can be in flight together), then the short path if the
-    // move is quiet, else the child is appended to the queue.
-    struct Cand {
-      u32 e, base;
-      Board pb;
-      u64 a;
-    };
-    auto fetch = [&](u32 e) {
-      const u32 pl = e >> 15;
-      return Cand{e, sh.base[pl], sh.par[pl], sh.att[pl]};
-    };
-    auto consume = [&](const Cand& c, bool live) {
-      const u32 pl = c.e >> 15;
-      const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
-      const u64 occ = occupied(c.pb);
-      const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
-      if (live && quiet) add(pl, c.base + ref_pawn_count_child<1 - STM>(c.pb, f, t), true);
-      const bool full = live && !quiet;
-      const u64 em = ballot(full);
-      if constexpr (PHASE == 7) {  // statistics: divide[0] quiet special children, [1] full-recount children
-        const u64 qm = ballot(live && quiet);
-        if (lane == 0) {
-          atomicAdd((unsigned long long*)divide, (unsigned long long)__popcll(qm));
-          atomicAdd((unsigned long long*)(divide + 1), (unsigned long long)__popcll(em));
+    c2c_group<STM, CAP, PHASE, BULK>(sh, valid, p, tag, divide);
+  }
+  tag_hist_flush(sh.hist, divide);
+}
+
+// ------------------------------------------------- K4: per-lane DFS (REF)
+// perft below a frontier level without materialising the deeper levels: every
+// lane walks the subtree of one frontier node depth first with an explicit
+// stack, and each node it reaches at L plies below the frontier is handed to
+// the block's c2c_group as a parent (the last two plies, bulk-counted as in
+// k_count2c).  Memory stays at the frontier level plus L - 1 stack frames per
+// lane, so perft(8), perft(9), ... need no level beyond ply 5 (a BFS level of
+// ply 7 of startpos alone is 3.3e9 nodes, ~112 GB).
+//
+// A lane's state is its top frame in registers -- the board being expanded,
+// the own pieces whose moves are still to come (srcs), the remaining targets
+// of the current piece f (tgts) -- with the frames above it in `stack`, SoA
+// [frame][field][lane] in HBM (coalesced; touched only on push and pop).
+// Moves are generated per piece (ref_piece_targets, chess.rs:199-360), so a
+// frame needs no move list.  Lanes take frontier nodes from one counter in
+// the run's result block (one atomic per wave per refill).
+struct DfsStack {
+  u64* frames;  // (L - 1) frames x 7 u64 (b0..b3, srcs, tgts, f) x lanes; null when L == 1
+  u64 lanes;    // grid x 256
+};
+
+template <int STM_P, u32 CAP, int L>
+__global__ __launch_bounds__(256, 3) void k_perft_dfs(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
+                                                      const Range* __restrict__ rng, u64* __restrict__ divide,
+                                                      u32* __restrict__ cursor, DfsStack stack) {
+  static_assert(L >= 1, "L = 0 is k_count2c");
+  constexpr u32 kStmF = (u32)(STM_P ^ (L & 1));  // side to move at the frontier ply
+  __shared__ C2cShared<CAP> sh;
+  tag_hist_init(sh.hist);
+  const u32 lane = lane_id();
+  const u64 gid = (u64)blockIdx.x * 256 + threadIdx.x;
+  const u64 lo = rng->lo, n_front = rng->hi - rng->lo;
+  int lvl = -1;  // frame of the board being expanded; -1: take a frontier node
+  bool done = false;
+  Board cb{0, 0, 0, 0};
+  u64 srcs = 0, tgts = 0;
+  int cf = 0;
+  u32 tag = 0;
+  auto own_of = [](const Board& b, u32 stm) { const u64 occ = occupied(b); return stm ? b.b0 : (occ & ~b.b0); };
+  auto frame = [&](int k, int field) -> u64& { return stack.frames[((u64)k * 7 + field) * stack.lanes + gid]; };
+  for (;;) {
+    Board p{0, 0, 0, 0};
+    bool valid = false;
+    while (!done && !valid) {
+      if (lvl < 0) {  // refill from the frontier: one atomic per wave
+        const u64 need = ballot(true);
+        const int leader = lsb(need);
+        u32 base = 0;
+        if ((int)lane == leader) base = atomicAdd(cursor, (u32)__popcll(need));
+        base = __shfl(base, leader, 64);
+        const u64 idx = (u64)base + (u64)__popcll(need & ((1ull << lane) - 1));
+        if (idx >= n_front) {
+          done = true;
+          break;
         }
+        cb = load_board(nodes, lo + idx);
+        tag = tags[lo + idx];
+        srcs = own_of(cb, kStmF);
+        tgts = 0;
+        lvl = 0;
+        continue;
       }
-      if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
-      qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
-    };
-    auto drain64 = [&]() {  // qn >= 64: recount 64 queued children in full
-      wave_lds_sync();
-      const u32 e2 = q[lane];
-      add(e2 >> 15, c2c_full<STM>(sh, e2), true);
-      wave_lds_sync();
-      if (lane + 64 < qn) q[lane] = q[lane + 64];
-      qn = __builtin_amdgcn_readfirstlane(qn - 64);
-    };
-    if constexpr (BULK && PHASE != 7) add(tid, (u32)simple_leaves, valid);
-    if constexpr (PHASE == 7) {  // [2] simple children, [3] parents
-      const u64 ns = wave_sum64(nsim), np = __popcll(ballot(valid));
-      if (lane == 0) {
-        atomicAdd((unsigned long long*)(divide + 2), (unsigned long long)ns);
-        atomicAdd((unsigned long long*)(divide + 3), (unsigned long long)np);
-      }
-    }
-    if constexpr (PHASE == 1 || PHASE == 2) acc += cnt + base + (u32)att;
-    for (u32 wbase = 0; wbase < (PHASE == 2 ? 0u : total); wbase += CAP) {
-      if (wbase) __syncthreads();  // previous window fully read
-      // each (f, t) of this parent's enumerated (BULK: special) moves -> visit(f, t)
-      auto each_move = [&](auto&& visit) {
-        if constexpr (BULK) ref_for_each_special<STM>(p, Fs, Ts, visit);
-        else ref_for_each_move<STM>(p, visit);
-      };
-      if (total <= CAP) {  // the norm: one window, no range checks
-        u32 j = excl;
-        if (valid) each_move([&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | (tid << 15); });
-      } else {
-        u32 j = excl;
-        if (valid && j < wbase + CAP && j + cnt > wbase) {
-          each_move([&](int f, int t) {
-            if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
-            ++j;
-          });
+      const u32 stm = kStmF ^ ((u32)lvl & 1);
+      if (tgts == 0) {
+        if (srcs == 0) {  // frame exhausted: pop
+          if (--lvl >= 0) {
+            cb = Board{frame(lvl, 0), frame(lvl, 1), frame(lvl, 2), frame(lvl, 3)};
+            srcs = frame(lvl, 4);
+            tgts = frame(lvl, 5);
+            cf = (int)frame(lvl, 6);
+          }
+          continue;
         }
+        cf = lsb(srcs);
+        srcs &= srcs - 1;
+        tgts = ref_piece_targets(cb, cf, stm, nibble(cb, cf) >> 1);
+        continue;
       }
-      __syncthreads();
-      const u32 nslots = min(CAP, total - wbase);
-      // two slots per lane per step, loaded together, so the LDS round trips overlap
-      u32 r0 = (PHASE == 1 || PHASE == 2) ? nslots : w * 64;
-      for (; r0 + 256 < nslots; r0 += 512) {
-        const u32 ra = r0 + lane, rb = r0 + 256 + lane;
-        const bool lb = rb < nslots;
-        const Cand ca = fetch(sh.slot[ra]);
-        const Cand cb = fetch(lb ? sh.slot[rb] : 0u);
-        consume(ca, true);
-        if (qn >= 64) drain64();
-        consume(cb, lb);
-        if (qn >= 64) drain64();
+      const int t = lsb(tgts);
+      tgts &= tgts - 1;
+      Board child = cb;
+      ref_make(child, cf, t);
+      if (lvl + 1 == L) {
+        p = child;
+        valid = true;
+        break;
       }
-      if (r0 < nslots) {
-        const u32 ra = r0 + lane;
-        const bool la = ra < nslots;
-        consume(fetch(la ? sh.slot[ra] : 0u), la);
-        if (qn >= 64) drain64();
+      if constexpr (L > 1) {  // push: the frame below the new top keeps its iterator
+        frame(lvl, 0) = cb.b0;
+        frame(lvl, 1) = cb.b1;
+        frame(lvl, 2) = cb.b2;
+        frame(lvl, 3) = cb.b3;
+        frame(lvl, 4) = srcs;
+        frame(lvl, 5) = tgts;
+        frame(lvl, 6) = (u64)cf;
+        ++lvl;
+        cb = child;
+        srcs = own_of(cb, stm ^ 1);
+        tgts = 0;
       }
     }
-    // drain this wave's queue (par/att of the chunk are still in LDS)
-    if (qn) {
-      wave_lds_sync();
-      const bool live = lane < qn;
-      const u32 e2 = live ? q[lane] : 0u;
-      const u32 k = live ? c2c_full<STM>(sh, e2) : 0u;
-      add(e2 >> 15, k, live);
-    }
-    tag_hist_add(sh.hist, tag0, acc, true);
-    __syncthreads();  // par/att/ptag/slot reused by the next chunk
+    if (__syncthreads_or(valid) == 0) break;  // every lane of the block is done
+    c2c_group<STM_P, CAP>(sh, valid, p, tag, divide);
   }
   tag_hist_flush(sh.hist, divide);
 }
@@ -937,6 +1059,33 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
   (void)waves;
   launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
 #endif
+}
+
+u64 dfs_lanes() {
+  return (u64)resident_grid(k_perft_dfs<0, 256 * 24, 1>, 256, kMaxGrid) * 256;
+}
+
+hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* nodes, const uint16_t* tags,
+                            const Range* rng, PerftResult* res, u64* stack_frames, u64 lanes) {
+  const DfsStack ds{stack_frames, lanes};
+  const u32 grid = (u32)(lanes / 256);
+#define DC_DFS(S, LL)                                                                                        \
+  hipLaunchKernelGGL((k_perft_dfs<S, 256 * 24, LL>), dim3(grid), dim3(256), 0, st, nodes, tags, rng, res->divide, \
+                     &res->dfs_next, ds)
+  if (L == 1) {
+    if (stm_parent) DC_DFS(1, 1);
+    else DC_DFS(0, 1);
+  } else if (L == 2) {
+    if (stm_parent) DC_DFS(1, 2);
+    else DC_DFS(0, 2);
+  } else if (L == 3) {
+    if (stm_parent) DC_DFS(1, 3);
+    else DC_DFS(0, 3);
+  } else {
+    return hipErrorNotSupported;
+  }
+#undef DC_DFS
+  return hipGetLastError();
 }
 
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,

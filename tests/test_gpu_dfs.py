@@ -1,0 +1,75 @@
+"""K4 -- per-lane DFS perft (k_perft_dfs) -- on the GPU through libdchess.so.
+
+Under RULES_REF a perft deeper than 7 keeps its BFS levels at ply <= 5 and
+walks the remaining L = depth - 7 plies above the two-ply final stage per
+lane with an explicit stack.  Checked against
+  * fastcpu (oracle/fastcpu.cpp) on sparse positions at depths 8, 9 and 10
+    (L = 1, 2, 3), computed in the test;
+  * the committed startpos perft(8) divide (tests/golden/ref_deep.json,
+    make_deep_golden.py), directly, sharded and through repeated device runs.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import dchess
+import oracle_lib as O
+
+pytestmark = pytest.mark.gpu
+
+DEEP = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "ref_deep.json")))
+
+SPARSE = [
+    ("4k3/8/8/8/8/8/8/R3K3 w - - 0 1", 8),       # L = 1
+    ("7k/8/8/8/3N4/8/8/K7 b - - 0 1", 8),        # L = 1, black to move at the root
+    ("7k/8/8/8/8/8/8/K7 w - - 0 1", 9),          # L = 2
+    ("8/8/2k5/8/8/5K2/8/8 b - - 0 1", 9),        # L = 2
+    ("k7/8/8/8/8/8/8/7K w - - 0 1", 10),         # L = 3
+]
+
+
+@pytest.mark.parametrize("fen,depth", SPARSE, ids=[f"d{d}-{i}" for i, (_, d) in enumerate(SPARSE)])
+def test_dfs_sparse_vs_fastcpu(engine, fen, depth):
+    p = O.Pos.from_fen(fen)
+    want, wdiv, wrm = O.fast_perft(p, depth, O.REF, threads=min(16, os.cpu_count() or 1))
+    tot, div, rm = engine.perft(dchess.pos_from_fen(fen), depth)
+    assert tot == want
+    assert dict(zip(rm.tolist(), div.tolist())) == dict(zip(wrm.tolist(), wdiv.tolist()))
+
+
+def test_perft8_startpos_golden(engine):
+    g = DEEP["startpos_d8"]
+    tot, div, rm = engine.perft(dchess.startpos(), 8)
+    assert tot == g["total"]
+    assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+
+
+@pytest.mark.parametrize("n_shards", [3, 8])
+def test_perft8_shards_sum(engine, n_shards):
+    s = dchess.startpos()
+    acc, t = None, 0
+    for k in range(n_shards):
+        st, sd, _ = engine.perft_shard(s, 8, 3, k, n_shards)
+        acc = sd.copy() if acc is None else acc + sd
+        t += st
+    assert t == DEEP["startpos_d8"]["total"]
+
+
+def test_perft8_repeat_device(engine):
+    s = dchess.startpos()
+    W, runs = 258, 2
+    buf = engine.alloc(runs * W * 8)
+    engine.perft_repeat_device(s, 8, 3, 0, 1, runs, buf)
+    engine.synchronize()
+    res = buf.download(np.uint64, runs * W).reshape(runs, W)
+    buf.free()
+    assert (res[:, 257] == DEEP["startpos_d8"]["total"]).all()
+    assert not (res[:, 256] >> np.uint64(32)).any()
+
+
+def test_depth_beyond_k4_unsupported(engine):
+    with pytest.raises(dchess.DChessError) as e:
+        engine.perft(dchess.startpos(), 11)
+    assert e.value.status == dchess.EUNSUPPORTED
