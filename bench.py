@@ -73,6 +73,7 @@ def parse():
     ap.add_argument("--hash-steps", type=int, default=3)
     ap.add_argument("--txs", type=int, default=262_144, help="signature leg: transactions per rank (0: off)")
     ap.add_argument("--tx-steps", type=int, default=3)
+    ap.add_argument("--only", default="", help="comma-separated legs to run (rocprof passes): " + ", ".join(LEGS))
     return ap.parse_args()
 
 
@@ -259,22 +260,44 @@ def _pmc(key):
     return json.load(open(pmc)).get(key)
 
 
-def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key):
-    """Bound: int32 VALU issue.  achieved = units/s x W, where W =
-    VALU lane-ops per unit executed by THIS kernel (rocprofv3 SQ_INSTS_VALU x 64
-    / units, committed under profiles/), so frac = the fraction of the VALU
-    issue peak the kernel runs at.  W_frozen (the first parity-passing kernel's
-    count) is reported beside it: rate x W_frozen / peak exceeds 1
-    once a kernel needs fewer ops per unit than the first one did."""
-    w = pmc_rec[w_key] if pmc_rec else w_frozen
+def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
+    """Bound: int32 VALU issue.  With W = VALU lane-ops per unit
+    executed by THIS kernel (rocprofv3 SQ_INSTS_VALU x 64 / units, committed
+    under profiles/) and the kernel's live rate (HIP events, units/s):
+      frac              = rate x W / peak: the fraction of the issue peak the
+                          kernel's VALU instructions occupy (full EXEC assumed);
+      frac_active_lanes = frac x VALUUtilization (SQ_THREAD_CYCLES_VALU /
+                          (SQ_ACTIVE_INST_VALU x 64)): lane-ops actually done;
+      frac_int          = rate x W_int / peak with W_int = (SQ_INSTS_VALU_INT32 +
+                          SQ_INSTS_VALU_INT64) x 64 / units: SURVEY §8d's and
+                          BASELINE.md §3's INT32 VALU fraction.
+    W_frozen (the first parity-passing kernel's W) is reported
+    beside them as the algorithmic gain W_frozen / W, not as a roofline."""
+    w = None
+    if pmc_rec:
+        w = pmc_rec.get("valu_lane_ops_per_unit") or (pmc_rec.get(w_key) if w_key else None)
+    measured = w is not None
+    w = w if measured else w_frozen
+    peak = VALU_PEAK_LANE_OPS
     roof = {"bound": "valu", "kernel": kernel, "unit": "TOPS (int32 VALU lane-ops/s)",
-            "achieved": rate * w / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
+            "achieved": rate * w / 1e12, "peak": peak / 1e12, "frac": rate * w / peak,
             f"W_lane_ops_per_{unit_name}": w,
-            "W_source": pmc_rec["source"] if pmc_rec else "frozen (no PMC record for this kernel)",
+            "W_source": pmc_rec["source"] if measured else "frozen (no PMC record for this kernel)",
             f"W_frozen_per_{unit_name}": w_frozen,
-            "frozen_W_frac": rate * w_frozen / VALU_PEAK_LANE_OPS,
-            "traffic": pmc_rec["hbm_bytes_per_launch"] if pmc_rec else None}
-    roof["frac"] = roof["achieved"] / roof["peak"]
+            "algorithmic_gain_vs_frozen_W": w_frozen / w if (w and w_frozen) else None,
+            "traffic": pmc_rec.get("hbm_bytes_per_launch") if pmc_rec else None}
+    if pmc_rec:
+        util = pmc_rec.get("valu_utilization")
+        w_int = pmc_rec.get("int_lane_ops_per_unit")
+        if util is not None:
+            roof["valu_utilization"] = util
+            roof["frac_active_lanes"] = roof["frac"] * util
+        if w_int is not None:
+            roof[f"W_int_lane_ops_per_{unit_name}"] = w_int
+            roof["frac_int"] = rate * w_int / peak
+        for k in ("lds_conflict_per_lds_cycle", "wait_frac", "salu_per_valu"):
+            if k in pmc_rec:
+                roof[k] = pmc_rec[k]
     return roof
 
 
@@ -386,6 +409,10 @@ def replay_leg(eng, d, args):
     out["end_to_end"] = {"value": tot_validated / e2e_dt, "unit": "validated moves/s",
                          "ms_per_step": 1e3 * e2e_dt / args.replay_steps, "gen_kernel_avg_ms": gen_ms,
                          "note": "each step generates the games on the device (k_gen_games_ref) and replays them"}
+    grec = _pmc("gen_games") if d.world == 1 else None
+    if grec and gen_ms > 0:
+        out["end_to_end"]["gen_roofline"] = valu_roof("k_gen_games_ref", st["validated"] / (gen_ms / 1e3), "move",
+                                                      None, grec)
     g = _golden_replay()
     want = (g.get("c4") if n_total == 10_000_000 else g.get("c5") if n_total == g.get("c5", {}).get("n_games") else None)
     parity = "no golden for this size"
@@ -457,6 +484,13 @@ def state_hash_leg(eng, d, args):
     eng.state_hash_device(d_moves, n, plies, d_names, d_off, d_h)
     eng.set_profiling(False)
     k = eng.kernel_stats("state_hash")
+    kms = k["total_ms"] / max(k["launches"], 1)
+    rec = _pmc("state_hash") if d.world == 1 else None
+    roof = valu_roof("k_state_hash_ref", n / (kms / 1e3), "game", None, rec) if rec else None
+    if roof is not None:
+        # HBM side: 160 B of moves (80 plies x u16) + ~12 B of names in, 32 B of hash out per game
+        roof["hbm"] = {"algorithmic_bytes_per_game": 2 * plies + 32 + 12,
+                       "achieved_GBps": n / (kms / 1e3) * (2 * plies + 44) / 1e9, "peak_GBps": HBM_PEAK_GBPS}
     h0 = d_h.download(np.uint8, 32)
     for b in (d_moves, d_h, d_names, d_off):
         b.free()
@@ -464,7 +498,7 @@ def state_hash_leg(eng, d, args):
     return {"value": total / dt, "unit": "game state hashes/s", "scaling": "weak",
             "workload": f"{n} seeded games x {plies} ply slots per rank: replay + serde_json(GameState) + keccak256 "
                         "per game (names white<g>/black<g>, start history \"\")",
-            "ms_per_step": 1e3 * dt / args.hash_steps, "kernel_avg_ms": k["total_ms"] / max(k["launches"], 1),
+            "ms_per_step": 1e3 * dt / args.hash_steps, "kernel_avg_ms": kms, "roofline": roof,
             "note": "inputs resident in HBM (moves, raw UTF-8 names); per call: device-side serde_json escaping of the "
                     "names (k_escape_len, scan, k_escape_write, one 8-byte readback) + the hash kernel",
             "first_hash": "0x" + bytes(h0).hex()}
@@ -514,11 +548,7 @@ def txsig_leg(eng, d, args):
            "ms_per_step": 1e3 * dt / args.tx_steps, "kernel_avg_ms": kms, "kernel_per_s": n / (kms / 1e3)}
     rec = _pmc("verify_tx")
     if rec and d.world == 1:
-        w = rec["valu_lane_ops_per_unit"]
-        out["roofline"] = {"bound": "valu", "kernel": "k_verify_tx", "unit": "TOPS (int32 VALU lane-ops/s)",
-                           "achieved": n / (kms / 1e3) * w / 1e12, "peak": VALU_PEAK_LANE_OPS / 1e12,
-                           "W_lane_ops_per_tx": w, "W_source": rec["source"],
-                           "frac": n / (kms / 1e3) * w / VALU_PEAK_LANE_OPS}
+        out["roofline"] = valu_roof("k_verify_tx", n / (kms / 1e3), "tx", None, rec)
     return out
 
 
@@ -548,6 +578,38 @@ def cpu_txsig(threads):
                       "core; the reference's libsecp256k1 could not be built here"}
 
 
+LEGS = ("perft", "perft6", "perft8", "replay", "hash", "tx", "latency")
+
+
+def perft8_leg(eng, d, args, pos):
+    """REF perft(startpos, 8) through K4 (k_perft_dfs: per-lane DFS below the ply-5
+    frontier), timed like the headline and checked against the committed golden
+    (tests/golden/ref_deep.json, fastcpu).  Secondary: the north star's explicit
+    per-lane-stack path."""
+    deep = os.path.join(REPO, "tests", "golden", "ref_deep.json")
+    want = json.load(open(deep)).get("startpos_d8", {}).get("total") if os.path.exists(deep) else None
+    if want is not None:
+        REF_STARTPOS[8] = want
+    steps = max(2, args.steps // 4)
+    leaves, dt = timed_perft(eng, d, args, pos, 8, steps, 1)
+    eng.reset_stats()
+    eng.set_profiling(True)
+    perft_step(eng, d, args, pos, 8)
+    d.sync()
+    eng.set_profiling(False)
+    k = eng.kernel_stats("dfs")
+    out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
+           "workload": "perft(startpos, 8) RULES_REF: BFS to ply 5, then K4 per-lane DFS (1 ply) + two-ply bulk final "
+                       "stage", "scaling": "strong", "leaves_per_step": leaves // steps,
+           "parity": "golden (fastcpu, tests/golden/ref_deep.json)" if want is not None else "no golden",
+           "dfs_kernel_ms": k["total_ms"] / max(k["launches"], 1)}
+    rec = _pmc("dfs_d8") if d.world == 1 else None
+    if rec and k["launches"]:
+        rate = k["units"] / max(k["launches"], 1) / (out["dfs_kernel_ms"] / 1e3)
+        out["roofline"] = valu_roof("k_perft_dfs", rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
+    return out
+
+
 def main():
     args = parse()
     d = Dist(args.gpus)
@@ -556,40 +618,66 @@ def main():
 
     if args.no_perft and not args.profile_only:
         raise SystemExit("--no-perft is only meaningful with --profile-only")
+    if args.only:
+        legs = set(args.only.split(","))
+        bad = legs - set(LEGS)
+        if bad:
+            raise SystemExit(f"--only: unknown legs {sorted(bad)} (known: {', '.join(LEGS)})")
+        args.profile_only = True
+    else:
+        legs = set(LEGS)
+        if args.no_perft:
+            legs -= {"perft"}
+        if args.profile_only:  # rocprof passes: headline (or replay + tx with --no-perft) only
+            legs -= {"perft6", "perft8", "hash", "latency"}
+            if not args.no_perft:
+                legs -= {"tx"}
+        if args.no_replay or args.games <= 0:
+            legs -= {"replay"}
+        if args.hash_games <= 0:
+            legs -= {"hash"}
+        if args.txs <= 0:
+            legs -= {"tx"}
+        if args.depth == 6:
+            legs -= {"perft6"}
     # ------------------------------------------------- perft (headline: depth 7)
-    p6 = None
-    if not args.no_perft:
+    p6 = p8 = None
+    leaves, dt, ks = 0, 0.0, None
+    if "perft" in legs:
         leaves, dt = timed_perft(eng, d, args, pos, args.depth, args.steps, args.warmup)
         ks = profiled_perft(eng, d, args, pos, args.depth, args.steps)
     # perft(6) (BASELINE configs[1]) on the same engine and method, secondary
-    if args.depth != 6 and not args.profile_only:
+    if "perft6" in legs:
         l6, dt6 = timed_perft(eng, d, args, pos, 6, 4 * args.steps, args.warmup)
         p6 = {"value": l6 / dt6, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt6 / (4 * args.steps),
               "steps": 4 * args.steps, "workload": "perft(startpos, 6) RULES_REF, frontier split at ply 3",
               "scaling": "strong"}
+    if "perft8" in legs:
+        p8 = perft8_leg(eng, d, args, pos)
 
     # --------------------------------------------------------------- replay
     replay = None
     replay_host = None
-    if not args.no_replay and args.games > 0:
+    if "replay" in legs:
         replay, replay_host = replay_leg(eng, d, args)
 
     # ------------------------------------------- state hash
     shash = None
-    if args.hash_games > 0 and not args.profile_only:
+    if "hash" in legs:
         shash = state_hash_leg(eng, d, args)
 
     # ------------------------------------ transaction signatures
     txsig = None
-    if args.txs > 0 and (not args.profile_only or args.no_perft):
+    if "tx" in legs:
         txsig = txsig_leg(eng, d, args)
 
-    v1 = validate_latency(eng) if not args.profile_only else None
-    if d.rank != 0 or args.profile_only:
+    v1 = validate_latency(eng) if "latency" in legs else None
+    if d.rank != 0 or (args.profile_only and not args.only):
         return
     line = {
         "metric": METRIC, "value": leaves / dt if dt > 0 else 0.0, "unit": "leaf nodes/s",
-        "n_gpus": d.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1e3 * dt / args.steps,
+        "n_gpus": d.world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": 1e3 * dt / args.steps if dt > 0 else None,
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "u64",
         "data": "synthetic (startpos tree; seeded random-legal games for replay)",
         "config": {"workload": f"perft(startpos, {args.depth}) RULES_REF (bit-exact with core/src/chess.rs), "
@@ -597,9 +685,12 @@ def main():
                                "per-root-move counts all-reduced over RCCL",
                    "depth": args.depth, "rules": "REF", "leaves_per_step": REF_STARTPOS.get(args.depth),
                    "parallelism": f"dp{d.world}"},
-        "roofline": roofline(ks, args.depth, d.world),
-        "kernels_ms_per_step": {k: v["total_ms"] / args.steps for k, v in ks.items()},
     }
+    if ks is not None:
+        line["roofline"] = roofline(ks, args.depth, d.world)
+        line["kernels_ms_per_step"] = {k: v["total_ms"] / args.steps for k, v in ks.items()}
+    if p8 is not None:
+        line["perft8"] = p8
     if p6 is not None:
         line["perft6"] = p6
     if shash is not None:

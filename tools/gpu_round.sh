@@ -32,27 +32,22 @@ if has balance; then
   timeout -k 10 200 python -u tools/shard_balance.py 7 > $O/balance.jsonl 2>&1 || { cat $O/balance.jsonl; exit 4; }
 fi
 if has pmc; then
-  rm -rf $O/pmc_*
-  P="--steps 3 --warmup 1 --no-cpu --profile-only"
-  pass() {  # $1 counters, $2 tag, $3.. bench args
-    local c=$1 t=$2; shift 2
-    step "pmc $t"
-    timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P "$@" > /dev/null 2>> $O/pmc.err
+  # 4 counter passes over every leg's kernels (one bench process per pass),
+  # then per-kernel records -> $O/pmc_latest.json (tools/pmc_summary.py)
+  rm -rf $O/pmc_p*
+  P="--steps 8 --warmup 1 --no-cpu --replay-steps 2 --hash-steps 1 --tx-steps 1 --only perft,perft8,replay,hash,tx"
+  pass() {  # $1 counters, $2 tag
+    step "pmc $2"
+    timeout -s KILL 240 rocprofv3 --pmc $1 --output-format csv -d $O/pmc_$2 -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err
   }
-  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" k1 --no-replay && \
-  pass "FETCH_SIZE" k2 --no-replay && pass "WRITE_SIZE" k3 --no-replay && \
-  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS GRBM_GUI_ACTIVE GRBM_COUNT" k4 --no-replay || { tail $O/pmc.err; exit 5; }
-  python tools/pmc_summary.py $O --json $O/pmc_perft.json --depth 7 --source "rocprofv3 --pmc, bench.py $P --no-replay" > $O/pmc_perft.txt
-  rm -rf $O/pmc_k*  # pass dirs only (pmc_perft.* must survive)
-  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" r1 --no-perft --replay-steps 2 && \
-  pass "FETCH_SIZE" r2 --no-perft --replay-steps 2 && pass "WRITE_SIZE" r3 --no-perft --replay-steps 2 || { tail $O/pmc.err; exit 6; }
-  U=$(python -c "import json;print(json.load(open('$O/bench.json'))['replay']['validated_per_step'])" 2>/dev/null || echo 0)
-  python tools/pmc_summary.py $O --json $O/pmc_replay.json --replay-units $U --source "rocprofv3 --pmc, bench.py $P --no-perft --replay-steps 2" > $O/pmc_replay.txt
-  python - <<'PY'
-import json
-a = json.load(open("gpurun_out/pmc_perft.json")); a.update(json.load(open("gpurun_out/pmc_replay.json")))
-json.dump(a, open("gpurun_out/pmc_latest.json", "w"), indent=1)
-PY
+  pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" p1 && \
+  pass "FETCH_SIZE" p2 && pass "WRITE_SIZE" p3 && \
+  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" p4 || { tail $O/pmc.err; exit 5; }
+  D8=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d8']['total'])")
+  python tools/pmc_summary.py $O --json $O/pmc_latest.json --source "rocprofv3 --pmc (4 passes), bench.py $P" \
+    --units "final_d7=k_count2c<=3282734510" --units "dfs_d8=k_perft_dfs<=$D8" \
+    --units "replay=k_replay_ref3=799999953" --units "gen_games=k_gen_games_ref=799999953" \
+    --units "state_hash=k_state_hash_ref=1000000" --units "verify_tx=k_verify_tx=262144" > $O/pmc_summary.txt
 fi
 if has txpmc; then
   rm -rf $O/pmc_t*

@@ -1,9 +1,24 @@
-"""Aggregates rocprofv3 --pmc CSVs (gpurun_out/pmc_*) per kernel, averaged per
-dispatch, and (with --json OUT --depth D --games N --plies P) writes the
-roofline inputs bench.py reads from profiles/pmc_latest.json:
-  hbm_bytes_per_launch = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B; the x2 is the
-  gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md "HBM [CDNA4]"), and
-  valu_lane_ops_per_unit = SQ_INSTS_VALU x 64 / units per dispatch."""
+"""Aggregates rocprofv3 --pmc CSVs (ROOT/pmc_*/) per kernel, averaged per
+dispatch, and (with --json OUT) writes the roofline inputs bench.py reads
+from profiles/pmc_latest.json.
+
+Per kernel record (units = the kernel's work units per dispatch, from --units):
+  hbm_bytes_per_launch   = 2 x FETCH_SIZE + WRITE_SIZE (KB -> B; the x2 is the
+                           gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md
+                           "HBM [CDNA4]")
+  valu_lane_ops_per_unit = SQ_INSTS_VALU x 64 / units         (issue: full EXEC assumed)
+  int_lane_ops_per_unit  = (SQ_INSTS_VALU_INT32 + _INT64) x 64 / units
+                           (SURVEY §8d / BASELINE.md §3: the INT32 VALU fraction)
+  valu_utilization       = SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)
+                           (rocprof's VALUUtilization: active lanes per VALU op)
+  lds_conflict_per_lds_cycle = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS
+  wait_frac              = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
+bench.py turns these into fractions of the 78.6 T lane-op/s issue peak with the
+kernel's live HIP-event time.
+
+--units takes KEY=PATTERN=UNITS triples, e.g. final_d7=k_count2c<=3282734510:
+the first kernel whose name contains PATTERN is written under KEY.
+"""
 import argparse
 import collections
 import csv
@@ -13,12 +28,9 @@ import json
 ap = argparse.ArgumentParser()
 ap.add_argument("root", nargs="?", default="gpurun_out")
 ap.add_argument("--json")
-ap.add_argument("--depth", type=int, default=7)
-ap.add_argument("--replay-units", type=float, default=0.0, help="validated moves per replay dispatch")
-ap.add_argument("--tx-units", type=float, default=0.0, help="transactions per k_verify_tx dispatch")
+ap.add_argument("--units", action="append", default=[], help="KEY=PATTERN=UNITS per dispatch")
 ap.add_argument("--source", default="")
 a = ap.parse_args()
-REF = {6: 120909581, 7: 3282734510}
 
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 disp = collections.defaultdict(set)
@@ -29,34 +41,51 @@ for d in sorted(glob.glob(f"{a.root}/pmc_*")):
             k = r["Kernel_Name"].split("(")[0].replace("void ", "")
             agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[(k, r["Counter_Name"])].add((d, r["Dispatch_Id"]))
-            meta[k] = (r["VGPR_Count"], r["Scratch_Size"], r["LDS_Block_Size"], r["Grid_Size"])
+            meta[k] = {"vgpr": r["VGPR_Count"], "scratch": r["Scratch_Size"], "lds": r["LDS_Block_Size"],
+                       "grid": r["Grid_Size"]}
 avg = {}
 for k, cs in agg.items():
     avg[k] = {c: v / max(1, len(disp[(k, c)])) for c, v in cs.items()}
-    print(k, "vgpr/scratch/lds/grid", meta[k])
+    print(k, meta[k])
     print("   ", {c: round(v) for c, v in sorted(avg[k].items())})
 
 
-def hbm(c):
-    if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
-        return None
-    return (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+def derived(c, units):
+    r = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        r["hbm_bytes_per_launch"] = (2 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024
+    if units:
+        if "SQ_INSTS_VALU" in c:
+            r["valu_lane_ops_per_unit"] = c["SQ_INSTS_VALU"] * 64 / units
+        if "SQ_INSTS_VALU_INT32" in c and "SQ_INSTS_VALU_INT64" in c:
+            r["int_lane_ops_per_unit"] = (c["SQ_INSTS_VALU_INT32"] + c["SQ_INSTS_VALU_INT64"]) * 64 / units
+    if c.get("SQ_ACTIVE_INST_VALU") and "SQ_THREAD_CYCLES_VALU" in c:
+        r["valu_utilization"] = c["SQ_THREAD_CYCLES_VALU"] / (c["SQ_ACTIVE_INST_VALU"] * 64)
+    if c.get("SQ_ACTIVE_INST_LDS") and "SQ_LDS_BANK_CONFLICT" in c:
+        r["lds_conflict_per_lds_cycle"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_ACTIVE_INST_LDS"]
+    if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_INST_ANY" in c:
+        r["wait_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    if c.get("SQ_INSTS_VALU") and "SQ_INSTS_SALU" in c:
+        r["salu_per_valu"] = c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"]
+    return r
 
 
 if a.json:
     out = {}
-    for k, c in avg.items():
-        if "k_count2b<dc::RefRules" in k or "k_count2c<" in k:  # the REF final stage
-            out[f"final_d{a.depth}"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
-                                          "valu_lane_ops_per_leaf": c.get("SQ_INSTS_VALU", 0) * 64 / REF[a.depth],
-                                          "counters_per_dispatch": c, "source": a.source}
-        if "k_replay_ref" in k and a.replay_units:
-            out["replay"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
-                             "valu_lane_ops_per_move": c.get("SQ_INSTS_VALU", 0) * 64 / a.replay_units,
-                             "counters_per_dispatch": c, "source": a.source}
-        if "k_verify_tx" in k and a.tx_units:
-            out["verify_tx"] = {"kernel": k, "hbm_bytes_per_launch": hbm(c),
-                                "valu_lane_ops_per_unit": c.get("SQ_INSTS_VALU", 0) * 64 / a.tx_units,
-                                "counters_per_dispatch": c, "source": a.source}
+    for spec in a.units:
+        key, pat, units = spec.split("=")
+        for k, c in avg.items():
+            if pat in k:
+                rec = {"kernel": k, "units_per_dispatch": float(units), "counters_per_dispatch": c,
+                       "resources": meta[k], "source": a.source}
+                rec.update(derived(c, float(units)))
+                # legacy names bench.py reads
+                if "valu_lane_ops_per_unit" in rec:
+                    rec["valu_lane_ops_per_leaf"] = rec["valu_lane_ops_per_move"] = rec["valu_lane_ops_per_unit"]
+                out[key] = rec
+                break
     json.dump(out, open(a.json, "w"), indent=1)
     print("wrote", a.json)
+    for key, rec in out.items():
+        print(key, {x: (round(v, 4) if isinstance(v, float) else v) for x, v in rec.items()
+                    if x not in ("counters_per_dispatch", "resources", "source", "kernel")})
