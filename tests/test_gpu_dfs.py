@@ -73,3 +73,32 @@ def test_depth_beyond_k4_unsupported(engine):
     with pytest.raises(dchess.DChessError) as e:
         engine.perft(dchess.startpos(), 11)
     assert e.value.status == dchess.EUNSUPPORTED
+
+
+# ------------------------------------------- refcpu-agreed deep pins (make_deep_golden.py)
+def test_startpos_d5_divide_pinned_by_refcpu(engine):
+    g = DEEP["startpos_d5"]
+    assert g["engines"] == ["refcpu", "fastcpu"]
+    tot, div, rm = engine.perft(dchess.startpos(), 5)
+    assert tot == g["total"]
+    assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+
+
+def test_startpos_d6_subtrees_pinned_by_refcpu(engine):
+    tot, div, rm = engine.perft(dchess.startpos(), 6)
+    got = {str(int(m)): int(v) for m, v in zip(rm, div)}
+    for m, v in DEEP["startpos_d6_subtrees"]["divide"].items():
+        assert got[m] == v
+
+
+def test_suite_d4_pinned_by_refcpu(engine):
+    for name, e in DEEP["suite_d4"]["positions"].items():
+        p = dchess.pos_from_fen(e["fen"])
+        for d, v in e["perft"].items():
+            assert engine.perft(p, int(d))[0] == v, (name, d)
+
+
+def test_random_d3_pinned_by_refcpu(engine):
+    for e in DEEP["random_d3"]["positions"]:
+        p = dchess.pos_from_cells(np.array(e["cells"], np.int8), e["stm"])
+        assert engine.perft(p, 3)[0] == e["perft3"]
