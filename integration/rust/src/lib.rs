@@ -64,6 +64,9 @@ extern "C" {
     pub fn dc_verify_tx_batch(ctx: *mut dc_ctx, strings: *const c_char, str_off: *const u32, actions: *const u32,
                               turns: *const i8, n: u32, verdicts: *mut u8) -> c_int;
     pub fn dc_sig_verdict_message(v: u8) -> *const c_char;
+    pub fn dc_replay_shard_range(n_games: u64, shard: u32, n_shards: u32, first: *mut u64, count: *mut u64) -> c_int;
+    pub fn dc_multi_replay(devices: *const c_int, n_devices: c_int, rules: u32, seed: u64, n_games: u64,
+                           n_plies: u32, noise_per_256: u32, bitmap: *mut u64, stats: *mut dc_replay_stats) -> c_int;
 }
 
 /// One device context (one gfx950 GPU, one HIP stream).  Not Sync: keep one per thread.

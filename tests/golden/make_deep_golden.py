@@ -72,7 +72,7 @@ def main():
         t0 = time.time()
         _, _, rm = O.fast_perft(start, 1, O.REF, threads=th)
         subs = {}
-        for m in (int(rm[0]), int(rm[-1])):  # a pawn push and the last knight move in fastcpu order
+        for m in (int(rm[0]), int(rm[-1])):  # the first and last root moves in fastcpu order (Nb1-a3, h2-h4)
             f, t = m & 63, (m >> 6) & 63
             v, cells, turn, _ = O.ref_apply(cells0, 0, "", f >> 3, f & 7, t >> 3, t & 7)
             assert v == 0

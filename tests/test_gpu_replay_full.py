@@ -87,3 +87,31 @@ def test_multi_replay_block_of_golden():
     bm, st = dchess.multi_replay([0], SEED, g["n_games"], GOLD["n_plies"], GOLD["noise_per_256"])
     assert st == g["stats"]
     assert sha(bm) == g["bitmap_sha256"]
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_replay_100m_c5_shards_vs_golden(engine, world):
+    """BASELINE configs[4]'s 100M-game batch as `world` replay shards (the
+    bench's rank layout at N = world, replayed here one shard after another on
+    one device), reassembled as dchess/dist.py does: whole-batch bitmap SHA-256
+    and combined counters == the C5 golden."""
+    import dchess.dist as D
+    g = GOLD["c5"]
+    n, plies = g["n_games"], GOLD["n_plies"]
+    words = (n + 63) // 64
+    whole = np.zeros((plies, words), np.uint64)
+    recs = []
+    for r in range(world):
+        first, cnt = D.replay_range(n, r, world)
+        w = (cnt + 63) // 64
+        d_moves, d_bm = engine.alloc(cnt * plies * 2), engine.alloc(w * plies * 8)
+        try:
+            engine.gen_games_device(d_moves, SEED, first, cnt, plies, GOLD["noise_per_256"])
+            st = engine.replay_device(d_moves, cnt, plies, d_bm, None)
+            whole[:, first // 64:first // 64 + w] = d_bm.download(np.uint64, w * plies).reshape(plies, w)
+        finally:
+            d_moves.free()
+            d_bm.free()
+        recs.append([st[k] for k in D.STAT_KEYS])
+    assert D.fold_stats(recs) == g["stats"]
+    assert sha(whole) == g["bitmap_sha256"]
