@@ -164,6 +164,30 @@ __device__ __forceinline__ int select_bit(u64 x, u32 k) {
   return base + __ffs(w) - 1;
 }
 
+// k-th (0-based) set bit of x without a data-dependent loop: five halving
+// steps on popcounts, then the last bit (x must have more than k bits set).
+__device__ __forceinline__ u32 select_bit_bf(u64 x, u32 k) {
+  u32 base = 0;
+  u32 w = (u32)x;
+  {
+    const u32 n = (u32)__popc(w);
+    const bool hi = k >= n;
+    k = hi ? k - n : k;
+    w = hi ? (u32)(x >> 32) : w;
+    base = hi ? 32u : 0u;
+  }
+#pragma unroll
+  for (u32 half = 16; half; half >>= 1) {
+    const u32 low = w & ((1u << half) - 1);
+    const u32 n = (u32)__popc(low);
+    const bool hi = k >= n;
+    k = hi ? k - n : k;
+    w = hi ? (w >> half) : low;
+    base += hi ? half : 0u;
+  }
+  return base;
+}
+
 // ---------------------------------------------------------------- wave ops
 __device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
 

@@ -383,8 +383,72 @@ __device__ __forceinline__ u32 ref_kth_move(const Board& b, u32 stm, u32 k) {
   return 0xFFFFu;  // unreachable when k < count
 }
 
+// K5, round 2.  The k-th move in (from, to) order without a per-piece loop:
+// every lane evaluates its position in the side-to-move view (white_view), so
+// one code path serves lanes of either colour; the source square of the k-th
+// move is found by a 6-step binary search over square prefixes, each step a
+// source-restricted bulk count (ref_count_from; prefix masks are built in real
+// square order and flipped into the view), and its target is the kk-th set bit
+// of that one piece's target set (ref_piece_targets_w).  The round-1 kernel
+// (k_gen_games_ref_v1: a per-piece loop with a per-kind switch) issued 3,842
+// VALU per wave and ply with 22 % of lanes active.  Same games, bit for bit
+// (tests/golden: C4 moves SHA-256).
 __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
                                                        u32 noise_per_256, uint16_t* __restrict__ out) {
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_games) return;
+  u64 s = seed ^ (first_game + g);
+  Board b{0, 0, 0, 0};
+  startpos_board(b);
+  u32 stm = 0;
+  bool over = false;
+  for (u32 ply = 0; ply < n_plies; ++ply) {
+    uint16_t* slot = out + (size_t)ply * n_games + g;
+    const Board w = view_sel(b, stm);
+    const u32 flip = stm ? 56u : 0u;
+    const Sides sw = sides<0>(w);
+    const Props pr = make_props(sw.empty);
+    const u32 n = over ? 0u : ref_count_from_w(sw, pr, ~0ull);
+    over = n == 0;
+    u64 r = 0;
+    if (!over) r = splitmix_next(s);
+    const bool noise = (u32)(r & 0xFF) < noise_per_256;
+    // the k-th move of the (from, to)-ordered list.  Own pieces in real square
+    // order p_0 < p_1 < ...; c(j) = #moves of p_0..p_{j-1}.  Games start at
+    // startpos and REF never adds a piece, so there are at most 16: four
+    // halving steps find the largest j with c(j) <= k.
+    const u32 k = (u32)(((r >> 32) * (u64)n) >> 32);
+    const u64 occ = occupied(b);
+    const u64 own = stm ? b.b0 : (occ & ~b.b0);
+    const u32 np = (u32)__popcll(own);
+    u32 lo = 0, clo = 0;
+#pragma unroll
+    for (u32 step = 8; step; step >>= 1) {
+      const u32 mid = lo + step;
+      const u64 real = mid < np ? ((1ull << select_bit_bf(own, mid)) - 1) : ~0ull;
+      const u64 view = stm ? flip_rows(real) : real;
+      const u32 c = (over || mid >= np) ? 0xFFFFFFFFu : ref_count_from_w(sw, pr, view);
+      if (c <= k) {
+        lo = mid;
+        clo = c;
+      }
+    }
+    const u32 f = over ? 0u : select_bit_bf(own, lo);
+    const u64 tv = ref_piece_targets_w(w, (int)(f ^ flip));
+    const u64 treal = stm ? flip_rows(tv) : tv;
+    const u32 kth = (n && k - clo < (u32)__popcll(treal)) ? (f | (select_bit_bf(treal, k - clo) << 6)) : 0u;
+    const u32 m = noise ? (u32)((r >> 8) & 0xFFF) : kth;
+    *slot = over ? (uint16_t)0xFFFF : (uint16_t)m;
+    const bool ok = !over && (!noise || ref_verdict(b, stm, m) == V_OK);
+    if (ok) {
+      ref_make(b, (int)(m & 63), (int)((m >> 6) & 63));
+      stm ^= 1;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_gen_games_ref_v1(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
+                                                          u32 noise_per_256, uint16_t* __restrict__ out) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_games) return;
   u64 s = seed ^ (first_game + g);
@@ -597,8 +661,13 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
 hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
                                 uint16_t* out) {
   if (n_games == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_gen_games_ref, dim3(blocks_for(n_games, 256)), dim3(256), 0, st, seed, first_game, n_games,
-                     n_plies, noise, out);
+  // DC_GEN=1 (A/B build only): the round-1 per-piece generator
+  static const bool v1 = [] {
+    const char* e = ab_env("DC_GEN");
+    return e && e[0] == '1';
+  }();
+  hipLaunchKernelGGL(v1 ? k_gen_games_ref_v1 : k_gen_games_ref, dim3(blocks_for(n_games, 256)), dim3(256), 0, st, seed,
+                     first_game, n_games, n_plies, noise, out);
   return hipGetLastError();
 }
 

@@ -88,8 +88,7 @@ __device__ __forceinline__ u32 king_moves(u64 k, u64 allowed) {
 // guards are applied on the target side so each leaper term is one shift, one
 // bitop3 (shifted & guard & ~own) and one popcount.
 template <int STM>
-__device__ __forceinline__ u32 ref_count(const Board& b) {
-  const Sides s = sides<STM>(b);
+__device__ __forceinline__ u32 ref_count_sides(const Sides& s) {
   typedef PawnDir<STM> PD;
   const u64 push1 = sh<PD::F>(s.P) & s.empty;
   const u64 push2 = and3(sh<PD::F>(push1), PD::ROW_DBL, s.empty);
@@ -109,6 +108,126 @@ __device__ __forceinline__ u32 ref_count(const Board& b) {
   c += pc(ray_moves<9, kNotA>(s.D, e, no)) + pc(ray_moves<-9, kNotH>(s.D, e, no));
   c += pc(ray_moves<7, kNotH>(s.D, e, no)) + pc(ray_moves<-7, kNotA>(s.D, e, no));
   return c;
+}
+
+template <int STM>
+__device__ __forceinline__ u32 ref_count(const Board& b) {
+  return ref_count_sides<STM>(sides<STM>(b));
+}
+
+// Moves of the side to move whose source lies in M (ref_count with every piece
+// class restricted to M; targets unrestricted).
+template <int STM>
+__device__ __forceinline__ u32 ref_count_from(const Board& b, u64 M) {
+  Sides s = sides<STM>(b);
+  s.P &= M;
+  s.N &= M;
+  s.K &= M;
+  s.D &= M;
+  s.O &= M;
+  return ref_count_sides<STM>(s);
+}
+
+// ------------------------------------------------ side-to-move view (k_gen_games_ref)
+// The REF rules are symmetric under a vertical flip that swaps the colours, so
+// any position can be evaluated as "White to move": rows reversed (byte swap,
+// square s -> s ^ 56) and, when Black is to move, the colour plane replaced
+// by the other side's pieces.  A wave whose lanes hold games with different
+// sides to move then runs one code path (ref_count<0>), not both.
+__device__ __forceinline__ u64 flip_rows(u64 x) { return __builtin_bswap64(x); }
+
+__device__ __forceinline__ Board white_view(const Board& b, u32 stm) {
+  if (!stm) return b;  // (callers keep this branch-free: see view_sel)
+  const u64 occ = occupied(b);
+  return Board{flip_rows(b.b0 ^ occ), flip_rows(b.b1), flip_rows(b.b2), flip_rows(b.b3)};
+}
+
+// Branch-free select of the two views (stm is per lane).
+__device__ __forceinline__ Board view_sel(const Board& b, u32 stm) {
+  const u64 occ = occupied(b);
+  const u64 m = 0ull - (u64)(stm & 1);
+  auto pick = [&](u64 a, u64 f) { return (a & ~m) | (f & m); };
+  return Board{pick(b.b0, flip_rows(b.b0 ^ occ)), pick(b.b1, flip_rows(b.b1)), pick(b.b2, flip_rows(b.b2)),
+               pick(b.b3, flip_rows(b.b3))};
+}
+
+// Slider propagators of one white-to-move board, per direction: the empty
+// squares (wrap-masked) and their 2- and 4-step products.  A source-restricted
+// count needs occluded fills from several generator subsets over ONE
+// occupancy (k_gen_games_ref's binary search), so the propagators are built
+// once per ply and each fill is then 3 shift/bitop3 steps.
+struct Props {
+  u64 p1[8], p2[8], p4[8];
+};
+
+template <int S, u64 M>
+__device__ __forceinline__ void prop_dir(u64 empty, u64& p1, u64& p2, u64& p4) {
+  p1 = empty & M;
+  p2 = p1 & sh<S>(p1);
+  p4 = p2 & sh<2 * S>(p2);
+}
+
+__device__ __forceinline__ Props make_props(u64 e) {
+  Props p;
+  prop_dir<8, kAll>(e, p.p1[0], p.p2[0], p.p4[0]);
+  prop_dir<-8, kAll>(e, p.p1[1], p.p2[1], p.p4[1]);
+  prop_dir<1, kNotA>(e, p.p1[2], p.p2[2], p.p4[2]);
+  prop_dir<-1, kNotH>(e, p.p1[3], p.p2[3], p.p4[3]);
+  prop_dir<9, kNotA>(e, p.p1[4], p.p2[4], p.p4[4]);
+  prop_dir<-9, kNotH>(e, p.p1[5], p.p2[5], p.p4[5]);
+  prop_dir<7, kNotH>(e, p.p1[6], p.p2[6], p.p4[6]);
+  prop_dir<-7, kNotA>(e, p.p1[7], p.p2[7], p.p4[7]);
+  return p;
+}
+
+template <int S, u64 M, int I>
+__device__ __forceinline__ u64 fill_props(u64 g, const Props& p, u64 allowed) {
+  g = or_and(g, p.p1[I], sh<S>(g));
+  g = or_and(g, p.p2[I], sh<2 * S>(g));
+  g = or_and(g, p.p4[I], sh<4 * S>(g));
+  return and3(sh<S>(g), M, allowed);
+}
+
+// ref_count<0> restricted to sources in Msrc, with the slider fills over the
+// precomputed propagators.
+__device__ __forceinline__ u32 ref_count_from_w(const Sides& s, const Props& pr, u64 Msrc) {
+  const u64 P = s.P & Msrc, N = s.N & Msrc, K = s.K & Msrc, D = s.D & Msrc, O = s.O & Msrc;
+  const u64 e = s.empty, no = s.notown;
+  const u64 push1 = sh<8>(P) & e;
+  u32 c = pc(push1) + pc(and3(sh<8>(push1), kRow(3), e));
+  c += pc(and3(sh<7>(P), kNotH, s.enemy)) + pc(and3(sh<9>(P), kNotA, s.enemy));
+  c += pc(and3(sh<17>(N), kNotA, no)) + pc(and3(sh<15>(N), kNotH, no));
+  c += pc(and3(sh<10>(N), kNotAB, no)) + pc(and3(sh<6>(N), kNotGH, no));
+  c += pc(and3(sh<-6>(N), kNotAB, no)) + pc(and3(sh<-10>(N), kNotGH, no));
+  c += pc(and3(sh<-15>(N), kNotA, no)) + pc(and3(sh<-17>(N), kNotH, no));
+  c += king_moves(K, no);
+  c += pc(fill_props<8, kAll, 0>(O, pr, no)) + pc(fill_props<-8, kAll, 1>(O, pr, no));
+  c += pc(fill_props<1, kNotA, 2>(O, pr, no)) + pc(fill_props<-1, kNotH, 3>(O, pr, no));
+  c += pc(fill_props<9, kNotA, 4>(D, pr, no)) + pc(fill_props<-9, kNotH, 5>(D, pr, no));
+  c += pc(fill_props<7, kNotH, 6>(D, pr, no)) + pc(fill_props<-7, kNotA, 7>(D, pr, no));
+  return c;
+}
+
+// Target set of the White piece on square f of a white-to-move board: every
+// piece class evaluated set-wise from the one-bit source (no branch on the
+// kind; the classes of other kinds come out empty).
+__device__ __forceinline__ u64 ref_piece_targets_w(const Board& b, int f) {
+  Sides s = sides<0>(b);
+  const u64 bit = 1ull << f;
+  const u64 P = s.P & bit, N = s.N & bit, K = s.K & bit, D = s.D & bit, O = s.O & bit;
+  const u64 e = s.empty, no = s.notown;
+  const u64 push1 = sh<8>(P) & e;
+  u64 t = push1 | and3(sh<8>(push1), kRow(3), e);
+  t |= ((sh<7>(P) & kNotH) | (sh<9>(P) & kNotA)) & s.enemy;
+  u64 l = (sh<17>(N) & kNotA) | (sh<15>(N) & kNotH) | (sh<10>(N) & kNotAB) | (sh<6>(N) & kNotGH);
+  l |= (sh<-6>(N) & kNotAB) | (sh<-10>(N) & kNotGH) | (sh<-15>(N) & kNotA) | (sh<-17>(N) & kNotH);
+  l |= sh<8>(K) | sh<-8>(K) | (sh<1>(K) & kNotA) | (sh<-1>(K) & kNotH) | (sh<9>(K) & kNotA) | (sh<7>(K) & kNotH) |
+       (sh<-7>(K) & kNotA) | (sh<-9>(K) & kNotH);
+  l |= ray_attacks<8, kAll>(O, e) | ray_attacks<-8, kAll>(O, e) | ray_attacks<1, kNotA>(O, e) |
+       ray_attacks<-1, kNotH>(O, e);
+  l |= ray_attacks<9, kNotA>(D, e) | ray_attacks<-9, kNotH>(D, e) | ray_attacks<7, kNotH>(D, e) |
+       ray_attacks<-7, kNotA>(D, e);
+  return t | (l & no);
 }
 
 // ------------------------------------------------ split count (k_count2c)
