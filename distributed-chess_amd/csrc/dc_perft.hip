@@ -1040,12 +1040,16 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
     return e ? std::atoi(e) : 0;
   }();
   // DC_C2C_WAVES (A/B): minimum waves per SIMD of the launch bounds, i.e. the
-  // VGPR budget.  4: 128 VGPRs with 116 B/lane of spills; 3 (default): 156
-  // VGPRs, no scratch.  perft(7) count2 time is the same (0.504 ms), perft(6)
-  // is 10 % faster with 3.
+  // VGPR budget.  4 (default since round 2): 128 VGPRs with 52 B/lane of
+  // spills; 3: 140 VGPRs, no scratch.  perft(7) count2: 0.498-0.505 vs
+  // 0.523-0.532 ms (tools/ab_phase.sh, round 2; round 1's body measured equal).
+  // Two round-2 dead ends: 16 instead of 24 slots per parent (LDS for 4
+  // blocks per CU) measured the same, and a chunk prefetch pipeline (next
+  // chunk's parents in registers across the group, next index fetched a group
+  // ahead) was slower at either budget (0.542 / 0.574 ms).
   static const int waves = [] {
     const char* e = ab_env("DC_C2C_WAVES");
-    return e ? std::atoi(e) : 3;
+    return e ? std::atoi(e) : 4;
   }();
 #ifdef DC_AB_KNOBS
   if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
@@ -1057,7 +1061,7 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
 #else
   (void)phase;
   (void)waves;
-  launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
+  launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
 #endif
 }
 
