@@ -103,36 +103,56 @@ __device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* wsum /*LDS[NW]*/, u
 // ------------------------------------------------------------- k_expand_top
 constexpr int kTopThreads = 1024;
 
+// Move slots of one top-level window in LDS: parent index << 15 | f | t << 6 | promo << 12.
+constexpr u32 kTopSlots = 9216;  // 36 KB: startpos ply 3 (8,902 children) in one window
+
+// One ply of the top expansion: counts per node, block scan, then in windows
+// of kTopSlots children: every thread writes its nodes' move words into LDS
+// at its scan offset, and all 1024 threads make and store one child per slot
+// (coalesced).  Making the children in the enumeration loop itself left ply
+// 3 to 400 threads making ~22 children each, one after another.
 template <class R, int STM>
 __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_meta, const uint16_t* cur_tags, u64 n,
                                           Board* nxt, uint16_t* nxt_meta, uint16_t* nxt_tags, u64 cap, bool root,
-                                          PerftResult* res, u64* wsum, u64* s_total) {
+                                          PerftResult* res, u64* wsum, u64* s_total, u32* slots) {
   const u32 t = threadIdx.x;
   const u64 k = (n + kTopThreads - 1) / kTopThreads;
   const u64 lo = min(n, (u64)t * k), hi = min(n, lo + k);
   u64 mine = 0;
   for (u64 i = lo; i < hi; ++i) mine += R::template count<STM>(cur[i], load_meta<R>(cur_meta, i));
   u64 total;
-  u64 o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);
+  const u64 o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);
   if (t == 0) *s_total = total;
   if (total > cap) return;  // caller flags overflow
-  for (u64 i = lo; i < hi; ++i) {
-    const Board p = cur[i];
-    const u32 pm = load_meta<R>(cur_meta, i);
-    const uint16_t tag = cur_tags[i];
-    R::template for_each<STM>(p, pm, [&](int f, int to, int promo) {
-      Board c = p;
-      const u32 cm = R::template make<STM>(c, pm, f, to, promo);
-      nxt[o] = c;
-      if constexpr (R::kMeta) nxt_meta[o] = (uint16_t)cm;
-      if (root) {
-        nxt_tags[o] = (uint16_t)o;
-        if (o < 256) res->root_moves[o] = (uint16_t)(f | (to << 6) | (promo << 12));
-      } else {
-        nxt_tags[o] = tag;
+  for (u64 wb = 0; wb < total; wb += kTopSlots) {
+    if (wb) __syncthreads();  // the previous window's slots are consumed
+    if (o < wb + kTopSlots && o + mine > wb) {
+      u64 j = o;
+      for (u64 i = lo; i < hi; ++i) {
+        R::template for_each<STM>(cur[i], load_meta<R>(cur_meta, i), [&](int f, int to, int promo) {
+          if (j >= wb && j < wb + kTopSlots) slots[j - wb] = ((u32)i << 15) | (u32)f | ((u32)to << 6) | ((u32)promo << 12);
+          ++j;
+        });
       }
-      ++o;
-    });
+    }
+    __syncthreads();
+    const u32 ns = (u32)min((u64)kTopSlots, total - wb);
+    for (u32 r = t; r < ns; r += kTopThreads) {
+      const u32 e = slots[r];
+      const u32 pl = e >> 15;
+      const int f = (int)(e & 63), to = (int)((e >> 6) & 63), promo = (int)((e >> 12) & 7);
+      Board c = cur[pl];
+      const u32 cm = R::template make<STM>(c, load_meta<R>(cur_meta, pl), f, to, promo);
+      const u64 oo = wb + r;
+      nxt[oo] = c;
+      if constexpr (R::kMeta) nxt_meta[oo] = (uint16_t)cm;
+      if (root) {
+        nxt_tags[oo] = (uint16_t)oo;
+        if (oo < 256) res->root_moves[oo] = (uint16_t)(f | (to << 6) | (promo << 12));
+      } else {
+        nxt_tags[oo] = cur_tags[pl];
+      }
+    }
   }
 }
 
@@ -154,6 +174,7 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
                                                              PerftResult* __restrict__ res, Range* __restrict__ out_rng) {
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
+  __shared__ u32 slots[kTopSlots];
   __shared__ uint16_t s_root_tag;
   __shared__ Board s_root;
   __shared__ uint16_t s_root_meta;
@@ -177,8 +198,10 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
     uint16_t* dm = last ? out_meta : sb.meta[ply - 1];
     uint16_t* dt = last ? out_tags : sb.tags[ply - 1];
     const u64 cap = last ? cap_out : sb.cap[ply - 1];
-    if ((stm0 ^ (ply - 1)) & 1) top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total);
-    else top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total);
+    if ((stm0 ^ (ply - 1)) & 1)
+      top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots);
+    else
+      top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots);
     __syncthreads();
     n = s_total;
     __syncthreads();
