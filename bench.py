@@ -87,12 +87,21 @@ class Dist:
         import torch
         self.torch = torch
         self.dist = None
+        # The engine's device: one GPU per rank.  DC_DIST_BACKEND=gloo (rehearsal
+        # only) runs the collectives on host tensors and lets several ranks share
+        # one GPU (device = local rank mod the devices present), so the N-rank
+        # code path -- shards, exchange steps, parity checks -- runs end to end
+        # on a one-GPU box; its timings mean nothing.
+        self.backend = os.environ.get("DC_DIST_BACKEND", "nccl")
+        n_dev = torch.cuda.device_count() if self.backend == "gloo" else 0
+        self.device = self.local % n_dev if n_dev else self.local
+        self.cdev = "cpu" if self.backend == "gloo" else f"cuda:{self.device}"
         # DC_FORCE_DIST=1: the RCCL path at world size 1 (torch.distributed.run
         # --nproc-per-node 1), to exercise it on a single-GPU box
         if self.world > 1 or os.environ.get("DC_FORCE_DIST") == "1":
             import torch.distributed as dist
-            torch.cuda.set_device(self.local)
-            dist.init_process_group("nccl")
+            torch.cuda.set_device(self.device)
+            dist.init_process_group(self.backend)
             self.dist = dist
 
     def sync(self):
@@ -104,14 +113,14 @@ class Dist:
     def allreduce_u64(self, arr):
         if self.dist is None:
             return arr
-        t = self.torch.tensor(arr.astype(np.int64), device=f"cuda:{self.local}")
+        t = self.torch.tensor(arr.astype(np.int64), device=self.cdev)
         self.dist.all_reduce(t)  # RCCL over xGMI
         return t.cpu().numpy().astype(np.uint64)
 
     def max(self, x):
         if self.dist is None:
             return x
-        t = self.torch.tensor([x], dtype=self.torch.float64, device=f"cuda:{self.local}")
+        t = self.torch.tensor([x], dtype=self.torch.float64, device=self.cdev)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
         return float(t.item())
 
@@ -227,14 +236,19 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup):
         totals = res[:, 257]
     else:
         torch = d.torch
-        t = torch.zeros((steps, W), dtype=torch.int64, device=f"cuda:{d.local}")
+        t = torch.zeros((steps, W), dtype=torch.int64, device=f"cuda:{d.device}")
         d.sync()
         t0 = time.perf_counter()
         eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, t.data_ptr())
         eng.synchronize()
         # the exchange step of every timed perft, bucketed: one RCCL all-reduce
         # (over xGMI) of all steps' per-root-move vectors, n_root words and totals
-        d.dist.all_reduce(t)
+        if d.cdev == "cpu":  # gloo rehearsal: the collective on a host copy
+            tc = t.cpu()
+            d.dist.all_reduce(tc)
+            t.copy_(tc)
+        else:
+            d.dist.all_reduce(t)
         d.sync()
         dt = d.max(time.perf_counter() - t0)
         res = t.cpu().numpy().view(np.uint64)
@@ -368,7 +382,7 @@ def replay_leg(eng, d, args):
     d_moves = eng.alloc(max(n * plies * 2, 2))
     d_dg = eng.alloc(max(n * 8, 8))
     # the bitmap is a torch tensor so the gather can read it in place (RCCL)
-    bm = torch.zeros((plies, max(w_r, 1)), dtype=torch.int64, device=f"cuda:{d.local}") if d.dist is not None \
+    bm = torch.zeros((plies, max(w_r, 1)), dtype=torch.int64, device=f"cuda:{d.device}") if d.dist is not None \
         else eng.alloc(max(plies * w_r * 8, 8))
     bm_ptr = bm.data_ptr() if d.dist is not None else bm
     seed = 0x5EED20241022
@@ -400,7 +414,7 @@ def replay_leg(eng, d, args):
     rk, gk = eng.kernel_stats("replay"), eng.kernel_stats("gen_games")
     # ---- exchange step + parity (after the timed region)
     stats, whole = D.combine_replay(st, bm if d.dist is not None else None, n_total, d.rank, d.world,
-                                    device=f"cuda:{d.local}")
+                                    device=d.cdev)
     tot_validated = stats["validated"] * args.replay_steps
     out = {"value": tot_validated / rdt, "unit": "validated moves/s",
            "workload": f"{n_total} seeded games x {plies} ply slots in total (seed 0x5EED20241022, 1/8 junk moves), "
@@ -619,7 +633,7 @@ def perft8_leg(eng, d, args, pos):
 def main():
     args = parse()
     d = Dist(args.gpus)
-    eng = dchess.Engine(d.local)
+    eng = dchess.Engine(d.device)
     pos = dchess.startpos()
 
     if args.no_perft and not args.profile_only:
