@@ -621,7 +621,10 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
 // counted per parent as n_simple x (base + pawn_O) and never enumerated; only
 // the other ("special") children go through the LDS slots.
 // PHASE (timing experiments only; wrong counts unless 0): 1 skips the children,
-// 2 also skips the enumeration, leaving the per-parent counts.  Phases other
+// 2 also skips the enumeration, leaving the per-parent counts; 5 skips the
+// full recounts (queued children still drained), 6 also the quiet children's
+// pawn counts; 7 replaces the counts by statistics (tools/c2c_stats.py);
+// 8 is 0 plus a per-block timeline (tools/c2c_trace.py).  Phases other
 // than 0 are instantiated only in the A/B build (-DDC_AB_KNOBS, libdchess_ab.so).
 // One group of 256 parents (one per thread; `valid` false for an empty slot):
 // the last two plies below each, added into the block's divide histogram.
@@ -687,7 +690,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
     const u64 occ = occupied(c.pb);
     const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
-    if (live && quiet) add(pl, c.base + ref_pawn_count_child<1 - STM>(c.pb, f, t), true);
+    if (live && quiet) add(pl, c.base + (PHASE == 6 ? (u32)t : ref_pawn_count_child<1 - STM>(c.pb, f, t)), true);
     const bool full = live && !quiet;
     const u64 em = ballot(full);
     if constexpr (PHASE == 7) {  // statistics: divide[0] quiet special children, [1] full-recount children
@@ -696,6 +699,26 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
         atomicAdd((unsigned long long*)divide, (unsigned long long)__popcll(qm));
         atomicAdd((unsigned long long*)(divide + 1), (unsigned long long)__popcll(em));
       }
+      // full children by the opponent O's slider group whose rays the move
+      // changes: [4] captures, [5] orthogonal only, [6] diagonal only, [7] both, [8] neither
+      const Sides so = sides<1 - STM>(c.pb);
+      const u64 e = so.empty;
+      const u64 ao = ray_attacks<8, kAll>(so.O, e) | ray_attacks<-8, kAll>(so.O, e) | ray_attacks<1, kNotA>(so.O, e) |
+                     ray_attacks<-1, kNotH>(so.O, e);
+      const u64 ad = ray_attacks<9, kNotA>(so.D, e) | ray_attacks<-9, kNotH>(so.D, e) | ray_attacks<7, kNotH>(so.D, e) |
+                     ray_attacks<-7, kNotA>(so.D, e);
+      const u64 ft = (1ull << f) | (1ull << t);
+      const bool capt = (occ >> t) & 1;
+      const bool go = (ao & ft) || ((so.O >> t) & 1), gd = (ad & ft) || ((so.D >> t) & 1);
+      const u64 m4 = ballot(full && capt), m5 = ballot(full && go && !gd), m6 = ballot(full && gd && !go);
+      const u64 m7 = ballot(full && go && gd), m8 = ballot(full && !go && !gd);
+      if (lane == 0) {
+        atomicAdd((unsigned long long*)(divide + 4), (unsigned long long)__popcll(m4));
+        atomicAdd((unsigned long long*)(divide + 5), (unsigned long long)__popcll(m5));
+        atomicAdd((unsigned long long*)(divide + 6), (unsigned long long)__popcll(m6));
+        atomicAdd((unsigned long long*)(divide + 7), (unsigned long long)__popcll(m7));
+        atomicAdd((unsigned long long*)(divide + 8), (unsigned long long)__popcll(m8));
+      }
     }
     if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
     qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
@@ -703,7 +726,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   auto drain64 = [&]() {  // qn >= 64: recount 64 queued children in full
     wave_lds_sync();
     const u32 e2 = q[lane];
-    add(e2 >> 15, c2c_full<STM>(sh, e2), true);
+    add(e2 >> 15, PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2), true);
     wave_lds_sync();
     if (lane + 64 < qn) q[lane] = q[lane + 64];
     qn = __builtin_amdgcn_readfirstlane(qn - 64);
@@ -762,29 +785,48 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     wave_lds_sync();
     const bool live = lane < qn;
     const u32 e2 = live ? q[lane] : 0u;
-    const u32 k = live ? c2c_full<STM>(sh, e2) : 0u;
+    const u32 k = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2)) : 0u;
     add(e2 >> 15, k, live);
   }
   tag_hist_add(sh.hist, tag0, acc, true);
   __syncthreads();  // par/att/ptag/slot reused by the next group
 }
 
+#ifdef DC_AB_KNOBS
+// PHASE 8 (A/B build): PHASE 0 plus a per-block timeline (wall clock, 100 MHz)
+// in g_c2c_trace, read back by dc_ab_c2c_trace (tools/c2c_trace.py).
+constexpr int kTraceWords = 8;
+constexpr int kTraceBlocks = 4096;
+__device__ u64 g_c2c_trace[kTraceBlocks * kTraceWords];
+#endif
+
 template <int STM, u32 CAP, int PHASE = 0, bool BULK = true, int MINW = 4>
 __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, u64* __restrict__ divide,
                                                  u32* __restrict__ next_chunk) {
   __shared__ C2cShared<CAP> sh;
+  constexpr int GP = PHASE == 8 ? 0 : PHASE;
+  [[maybe_unused]] u64 t_entry = 0, t_wait = 0, t_last = 0, n_chunks = 0;
+  if constexpr (PHASE == 8) t_entry = wall_clock64();
   tag_hist_init(sh.hist);
   const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
   // Blocks take 256-parent chunks from a counter: the cost of a chunk varies
   // with its positions, and static ranges left the slowest block behind (a
-  // sharded launch has only ~3 chunks per block).
+  // sharded launch has only ~3 chunks per block).  The counter's round trips
+  // are 2.7 % of a block's lifetime at perft(7) (tools/c2c_trace.py).
   for (;;) {
+    [[maybe_unused]] u64 ta = 0;
+    if constexpr (PHASE == 8) ta = wall_clock64();
     if (tid == 0) sh.next = atomicAdd(next_chunk, 1u);
     __syncthreads();
+    if constexpr (PHASE == 8) {
+      t_last = wall_clock64();
+      t_wait += t_last - ta;
+    }
     const u64 s = lo + (u64)sh.next * kChunk;
     if (s >= hi) break;  // block-uniform
+    if constexpr (PHASE == 8) ++n_chunks;
     const u64 i = s + tid;
     const bool valid = i < hi;
     Board p{0, 0, 0, 0};
@@ -793,9 +835,26 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
       p = load_board(nodes, i);
       tag = tags[i];
     }
-    c2c_group<STM, CAP, PHASE, BULK>(sh, valid, p, tag, divide);
+    c2c_group<STM, CAP, GP, BULK>(sh, valid, p, tag, divide);
   }
   tag_hist_flush(sh.hist, divide);
+#ifdef DC_AB_KNOBS
+  if constexpr (PHASE == 8) {
+    if (tid == 0 && blockIdx.x < kTraceBlocks) {
+      u32 xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      u64* r = g_c2c_trace + blockIdx.x * kTraceWords;
+      r[0] = t_entry;
+      r[1] = wall_clock64();
+      r[2] = n_chunks;
+      r[3] = t_wait;
+      r[4] = xcc & 15;
+      r[5] = t_last;
+      r[6] = gridDim.x;
+      r[7] = 0;
+    }
+  }
+#endif
 }
 
 // ------------------------------------------------- K4: per-lane DFS (REF)
@@ -1078,7 +1137,10 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
   if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 5) launch_count2c_cap<256 * 24, 5, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 6) launch_count2c_cap<256 * 24, 6, true>(st, stm, nodes, tags, rng, divide);
   else if (phase == 7) launch_count2c_cap<256 * 24, 7, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 8) launch_count2c_cap<256 * 24, 8, true>(st, stm, nodes, tags, rng, divide);
   else if (waves == 4) launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
   else launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
 #else
@@ -1087,6 +1149,18 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
   launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
 #endif
 }
+
+#ifdef DC_AB_KNOBS
+// A/B build only: the last PHASE 8 launch's per-block timeline
+// (kTraceWords u64 per block: entry, exit, chunks, counter-wait ticks, XCC id,
+// last counter return, grid size).
+extern "C" __attribute__((visibility("default"))) int dc_ab_c2c_trace(u64* out, u64 n_words) {
+  const u64 n = std::min<u64>(n_words, (u64)kTraceBlocks * kTraceWords);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c2c_trace), n * sizeof(u64), 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
 
 u64 dfs_lanes() {
   return (u64)resident_grid(k_perft_dfs<0, 256 * 24, 1>, 256, kMaxGrid) * 256;
