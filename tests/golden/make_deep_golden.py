@@ -1,7 +1,7 @@
 """Deep REF perft pins -- TEST INFRASTRUCTURE.
 
 Run:  python tests/golden/make_deep_golden.py [--threads 8] [--max-depth 9]
-      (refcpu pins ~10 min on 8 cores; fastcpu perft(8) ~2 min, perft(9) ~1 h)
+      (refcpu pins ~10 min on 8 cores; fastcpu perft(8) ~10 min, perft(9) ~2.5 h)
 
 Round 1 pinned REF perft beyond depth 4 only by fastcpu (the mailbox engine),
 tied to refcpu -- the literal restatement of /root/reference/core/src/chess.rs

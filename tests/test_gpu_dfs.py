@@ -69,6 +69,16 @@ def test_perft8_repeat_device(engine):
     assert not (res[:, 256] >> np.uint64(32)).any()
 
 
+def test_perft9_startpos_golden(engine):
+    """perft(startpos, 9) through K4 at L = 2 (explicit per-lane stack of one
+    frame): total and divide against fastcpu's golden (2.6e12 leaves, 2.5 h on
+    8 host threads; ~0.6 s here).  The BFS levels stop at ply 5 (167 MB)."""
+    g = DEEP["startpos_d9"]
+    tot, div, rm = engine.perft(dchess.startpos(), 9)
+    assert tot == g["total"] == 2_597_923_551_373
+    assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+
+
 def test_depth_beyond_k4_unsupported(engine):
     with pytest.raises(dchess.DChessError) as e:
         engine.perft(dchess.startpos(), 11)
