@@ -106,43 +106,85 @@ constexpr int kTopThreads = 1024;
 // Move slots of one top-level window in LDS: parent index << 15 | f | t << 6 | promo << 12.
 constexpr u32 kTopSlots = 9216;  // 36 KB: startpos ply 3 (8,902 children) in one window
 
+#ifdef DC_AB_KNOBS
+// A/B build: k_expand_top's timeline (wall clock, 100 MHz): per ply the ticks
+// at entry, after the counts, after the scan, after the enumeration, at exit.
+__device__ u64 g_top_trace[4 * 5];
+#define DC_TOP_STAMP(ply, k) \
+  do {                       \
+    if (threadIdx.x == 0 && (ply) < 4) g_top_trace[(ply) * 5 + (k)] = wall_clock64(); \
+  } while (0)
+#else
+#define DC_TOP_STAMP(ply, k) \
+  do {                       \
+  } while (0)
+#endif
+
+// Nodes of a top-level ply staged in LDS (parents read per child without a
+// global round trip) when the ply holds at most this many (startpos ply 2: 400).
+constexpr u32 kTopStage = 512;
+
 // One ply of the top expansion: counts per node, block scan, then in windows
 // of kTopSlots children: every thread writes its nodes' move words into LDS
 // at its scan offset, and all 1024 threads make and store one child per slot
 // (coalesced).  Making the children in the enumeration loop itself left ply
-// 3 to 400 threads making ~22 children each, one after another.
+// 3 to 400 threads making ~22 children each, one after another.  A ply of at
+// most kTopStage nodes is staged in LDS (spar/smeta/stags) as it is counted,
+// so the enumeration and the children read their parents from LDS: reading
+// them from the previous ply's global output cost a dependent L2 round trip
+// per child (9 per thread at ply 3).
 template <class R, int STM>
 __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_meta, const uint16_t* cur_tags, u64 n,
                                           Board* nxt, uint16_t* nxt_meta, uint16_t* nxt_tags, u64 cap, bool root,
-                                          PerftResult* res, u64* wsum, u64* s_total, u32* slots) {
+                                          PerftResult* res, u64* wsum, u64* s_total, u32* slots, Board* spar,
+                                          uint16_t* smeta, uint16_t* stags, u32 ply) {
   const u32 t = threadIdx.x;
+  DC_TOP_STAMP(ply, 0);
+  const bool stage = n <= kTopStage;
   const u64 k = (n + kTopThreads - 1) / kTopThreads;
   const u64 lo = min(n, (u64)t * k), hi = min(n, lo + k);
   u64 mine = 0;
-  for (u64 i = lo; i < hi; ++i) mine += R::template count<STM>(cur[i], load_meta<R>(cur_meta, i));
+  for (u64 i = lo; i < hi; ++i) {
+    const Board bi = cur[i];
+    const u32 mi = load_meta<R>(cur_meta, i);
+    if (stage) {
+      spar[i] = bi;
+      if constexpr (R::kMeta) smeta[i] = (uint16_t)mi;
+      stags[i] = root ? (uint16_t)0 : cur_tags[i];
+    }
+    mine += R::template count<STM>(bi, mi);
+  }
+  DC_TOP_STAMP(ply, 1);
   u64 total;
-  const u64 o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);
+  const u64 o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);  // its barriers publish the staging
+  DC_TOP_STAMP(ply, 2);
   if (t == 0) *s_total = total;
   if (total > cap) return;  // caller flags overflow
+  const Board* par = stage ? spar : cur;
+  auto pmeta = [&](u64 i) -> u32 {
+    if constexpr (R::kMeta) return stage ? smeta[i] : cur_meta[i];
+    else return 0;
+  };
   for (u64 wb = 0; wb < total; wb += kTopSlots) {
     if (wb) __syncthreads();  // the previous window's slots are consumed
     if (o < wb + kTopSlots && o + mine > wb) {
       u64 j = o;
       for (u64 i = lo; i < hi; ++i) {
-        R::template for_each<STM>(cur[i], load_meta<R>(cur_meta, i), [&](int f, int to, int promo) {
+        R::template for_each<STM>(par[i], pmeta(i), [&](int f, int to, int promo) {
           if (j >= wb && j < wb + kTopSlots) slots[j - wb] = ((u32)i << 15) | (u32)f | ((u32)to << 6) | ((u32)promo << 12);
           ++j;
         });
       }
     }
     __syncthreads();
+    DC_TOP_STAMP(ply, 3);
     const u32 ns = (u32)min((u64)kTopSlots, total - wb);
     for (u32 r = t; r < ns; r += kTopThreads) {
       const u32 e = slots[r];
       const u32 pl = e >> 15;
       const int f = (int)(e & 63), to = (int)((e >> 6) & 63), promo = (int)((e >> 12) & 7);
-      Board c = cur[pl];
-      const u32 cm = R::template make<STM>(c, load_meta<R>(cur_meta, pl), f, to, promo);
+      Board c = par[pl];
+      const u32 cm = R::template make<STM>(c, pmeta(pl), f, to, promo);
       const u64 oo = wb + r;
       nxt[oo] = c;
       if constexpr (R::kMeta) nxt_meta[oo] = (uint16_t)cm;
@@ -150,7 +192,7 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
         nxt_tags[oo] = (uint16_t)oo;
         if (oo < 256) res->root_moves[oo] = (uint16_t)(f | (to << 6) | (promo << 12));
       } else {
-        nxt_tags[oo] = cur_tags[pl];
+        nxt_tags[oo] = stage ? stags[pl] : cur_tags[pl];
       }
     }
   }
@@ -175,6 +217,9 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
   __shared__ u32 slots[kTopSlots];
+  __shared__ Board spar[kTopStage];
+  __shared__ uint16_t smeta[R::kMeta ? kTopStage : 1];
+  __shared__ uint16_t stags[kTopStage];
   __shared__ uint16_t s_root_tag;
   __shared__ Board s_root;
   __shared__ uint16_t s_root_meta;
@@ -199,10 +244,13 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
     uint16_t* dt = last ? out_tags : sb.tags[ply - 1];
     const u64 cap = last ? cap_out : sb.cap[ply - 1];
     if ((stm0 ^ (ply - 1)) & 1)
-      top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots);
+      top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots, spar, smeta,
+                      stags, ply);
     else
-      top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots);
+      top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots, spar, smeta,
+                      stags, ply);
     __syncthreads();
+    DC_TOP_STAMP(ply, 4);
     n = s_total;
     __syncthreads();
     bool bad = n > cap;
@@ -288,7 +336,8 @@ __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restric
 // compacted into LDS slots at block-scan offsets, then every lane makes one
 // child per round and stores it at chunk_base + slot -- consecutive lanes write
 // consecutive nodes (coalesced), and a ~200k-node ply keeps all lanes busy.
-constexpr u32 kWriteCap = 256 * 30;  // ply-5 chunks of perft(7) average 24.8 children per parent: one window
+constexpr u32 kWriteCap = 256 * 30;
+constexpr u32 kWriteSplit = 16;  // at most this many blocks share one chunk  // ply-5 chunks of perft(7) average 24.8 children per parent: one window
 
 struct WriteShared {
   Board par[256];
@@ -308,7 +357,14 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
   const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
   const u64 nch = (hi - lo + kChunk - 1) / kChunk;
-  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
+  // A level of few chunks (startpos ply 4: 35) would leave most of the
+  // resident grid idle with each block making ~5,600 children in ~22 rounds:
+  // then S blocks share a chunk, each enumerating its moves but making only
+  // its S-th of every window's children.
+  const u32 S = (u32)max<u64>(1, min<u64>(kWriteSplit, gridDim.x / max<u64>(nch, 1)));
+  for (u64 item = blockIdx.x; item < nch * S; item += gridDim.x) {
+    const u64 c = item / S;
+    const u32 part = (u32)(item % S);
     const u64 i = lo + c * kChunk + tid;
     const bool valid = i < hi;
     const u32 cnt = valid ? counts[i - lo] : 0;
@@ -325,17 +381,20 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
       if constexpr (R::kMeta) sh.pmeta[tid] = pm;
       sh.ptag[tid] = tags[i];
     }
-    for (u32 base = 0; base < total; base += kWriteCap) {
-      if (base) __syncthreads();  // previous window fully consumed
+    for (u32 wb = 0; wb < total; wb += kWriteCap) {
+      if (wb) __syncthreads();  // previous window fully consumed
+      // this block's part of the window: children [base, base + nslots)
+      const u32 nw = min(kWriteCap, total - wb);
+      const u32 base = wb + (u32)((u64)nw * part / S);
+      const u32 nslots = wb + (u32)((u64)nw * (part + 1) / S) - base;
       u32 j = excl;
-      if (valid && j < base + kWriteCap && j + cnt > base) {
+      if (valid && j < base + nslots && j + cnt > base) {
         R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
-          if (j >= base && j - base < kWriteCap) sh.slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (tid << 15);
+          if (j >= base && j - base < nslots) sh.slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (tid << 15);
           ++j;
         });
       }
       __syncthreads();
-      const u32 nslots = min(kWriteCap, total - base);
       for (u32 r = tid; r < nslots; r += 256) {
         const u64 o = base_out + base + r;
         if (o >= cap) continue;
@@ -1157,6 +1216,14 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
 extern "C" __attribute__((visibility("default"))) int dc_ab_c2c_trace(u64* out, u64 n_words) {
   const u64 n = std::min<u64>(n_words, (u64)kTraceBlocks * kTraceWords);
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c2c_trace), n * sizeof(u64), 0, hipMemcpyDeviceToHost) == hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+#ifdef DC_AB_KNOBS
+extern "C" __attribute__((visibility("default"))) int dc_ab_top_trace(u64* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_top_trace), sizeof(g_top_trace), 0, hipMemcpyDeviceToHost) == hipSuccess
              ? 0
              : -1;
 }
