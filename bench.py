@@ -322,9 +322,10 @@ def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
 
 
 def replay_roof(kr, n_games):
-    """k_replay_ref3 (DC_REPLAY=1: k_replay_ref).  HBM: 2 B in (u16 move) + 1/8 B
-    out (accept bit) per validated move, plus 8 B of digest per game."""
-    kernel = "k_replay_ref" if (os.environ.get("DCHESS_LIB") and os.environ.get("DC_REPLAY") == "1") else "k_replay_ref3"
+    """k_replay_ref4 (A/B build: DC_REPLAY=1 k_replay_ref, =3 k_replay_ref3).  HBM: 2 B in
+    (u16 move) + 1/8 B out (accept bit) per validated move, plus 8 B of digest per game."""
+    ab = os.environ.get("DC_REPLAY") if os.environ.get("DCHESS_LIB") else None
+    kernel = {"1": "k_replay_ref", "3": "k_replay_ref3"}.get(ab, "k_replay_ref4")
     rec = _pmc("replay")
     if rec and rec.get("kernel", "").split("<")[0].replace("dc::", "") != kernel:
         rec = None

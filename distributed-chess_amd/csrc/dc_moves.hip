@@ -366,6 +366,165 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref3(Mailbox mb0, u64 occ
   }
 }
 
+// ------------------------------------------- replay, round 3 (k_replay_ref4)
+// k_replay_ref3's table + mailbox scheme with the per-ply issue trimmed
+// (profiles/r02: ref3 issued 45 VALU + 23 SALU per wave and ply and waited 36 %
+// of its cycles):
+//   - the four LDS reads of a ply (btw, geo, the f and t mailbox dwords) issue
+//     together: ref3's `okb && (btw & occ) == 0` let the compiler sink the btw
+//     read behind a branch, a second dependent LDS round trip per ply plus an
+//     exec-mask save/restore;
+//   - one buffer descriptor spans the whole ply-major move array (the launcher
+//     takes this kernel when it is < 4 GiB) and a ply's row is the SGPR
+//     soffset min(p, last) * row_bytes: 2 SALU per load instead of 8;
+//   - inactive lanes (the last chunk only) replay game n-1 unmasked: their
+//     counters are dropped per chunk and their bitmap bits masked at the
+//     64-ply store, so no per-ply select;
+//   - both ballot halves go into the lanes' words under one M0 write.
+__global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ0, u32 stm0, const uint16_t* __restrict__ moves,
+                                                           u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
+                                                           u64* __restrict__ digests, u64* __restrict__ partial) {
+  __shared__ __attribute__((aligned(16))) unsigned char r4_smem[kR3TabBytes + kR3MbBytes];
+  u64* btw = reinterpret_cast<u64*>(r4_smem);
+  u32* mb = reinterpret_cast<u32*>(r4_smem + kR3TabBytes);
+  const u32 tid = threadIdx.x;
+  for (u32 e = tid; e < 4096; e += kR3Threads) {
+    btw[e] = between((int)(e & 63), (int)(e >> 6));
+    reinterpret_cast<u32*>(r4_smem + 4096 * 8)[e] = replay_geo(e);
+  }
+  __syncthreads();
+  const u32 lane = lane_id();
+  const u32 words = (n_games + 63) >> 6;
+  const u32 tid4 = tid * 4;
+  const u32 last = n_plies - 1;
+  const u32 row_bytes = n_games * 2;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)moves, 0, n_plies * row_bytes, 0x00020000);
+  u32* my = mb + tid;
+  u32 validated = 0, accepted = 0;
+  u64 dsum = 0, dxor = 0;
+  for (u32 round = 0;; ++round) {
+    const u32 c = (round * gridDim.x + blockIdx.x) * (kR3Threads / 64) + (tid >> 6);
+    if (c >= words) break;
+    const u32 g = (c << 6) | lane;
+    const bool active = g < n_games;
+    const u64 amask = ballot(active);
+    const u32 goff = (active ? g : n_games - 1) * 2;
+    auto load_move = [&](u32 p) -> u32 {
+      return __builtin_amdgcn_raw_buffer_load_b16(rs, goff, min(p, last) * row_bytes, 0);
+    };
+#pragma unroll
+    for (u32 j = 0; j < 8; ++j) my[j * kR3Threads] = mb0.d[j];
+    u64 occ = occ0;
+    u32 stm = stm0;
+    u32 nval = 0, nacc = 0;
+    u32 buf[kReplayPrefetch];
+#pragma unroll
+    for (int k = 0; k < kReplayPrefetch; ++k) buf[k] = load_move((u32)k);
+    u32 bw_lo = 0, bw_hi = 0;  // lane j holds the ballot word of ply 64q + j
+    auto ply_step = [&](u32 m, u32 slot) {
+      const u32 m2 = m << 2, m3 = m << 3;
+      const u32 af = __builtin_amdgcn_bitop3_b32(m << 9, tid4, 0x7000u, 0xE4);
+      const u32 at = __builtin_amdgcn_bitop3_b32(m3, tid4, 0x7000u, 0xE4);
+      const u64 bt = *reinterpret_cast<const u64*>(r4_smem + (m3 & 0x7FF8u));
+      const u32 gw = *reinterpret_cast<const u32*>(r4_smem + 4096 * 8 + (m2 & 0x3FFCu));
+      const u32 wf = *reinterpret_cast<const u32*>(r4_smem + kR3TabBytes + af);
+      const u32 wt = *reinterpret_cast<const u32*>(r4_smem + kR3TabBytes + at);
+      const u32 st = (m >> 4) & 28;
+      const u32 nib = __builtin_amdgcn_ubfe(wf, m2, 4);
+      const u32 nibt = __builtin_amdgcn_ubfe(wt, st, 4);
+      const u32 x = nibt ^ stm;
+      const u32 shift = nib | (__builtin_amdgcn_ubfe(kEnemyLut, x, 1) << 4);
+      const u32 geo_ok = __builtin_amdgcn_ubfe(gw, shift, 1), own = __builtin_amdgcn_ubfe(kOwnLut, x, 1);
+      const u32 okb = __builtin_amdgcn_bitop3_b32(geo_ok, own, __builtin_amdgcn_bitop3_b32(nib, stm, m >> 15, 0xBE), 0x10);
+      // okb has only bit 0; blocked != 0 iff a square between f and t is
+      // occupied, so ok = blocked < okb is one compare (the btw read issues
+      // with the other three for every lane)
+      const u32 blocked = __builtin_amdgcn_bitop3_b32((u32)bt, (u32)occ, (u32)(bt >> 32) & (u32)(occ >> 32), 0xEA);  // (a & b) | c
+      const bool ok = blocked < okb;
+      const u64 w = ballot(ok);
+      // the lanes' ballot words are written before the make-move branch, so the
+      // compare's own mask feeds both (no mask rematerialised after the branch)
+      asm volatile("s_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
+                   : "+v"(bw_lo), "+v"(bw_hi)
+                   : "s"((u32)w), "s"((u32)(w >> 32)), "s"(slot)
+                   : "m0");
+      if (ok) {
+        atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + af), nib << m2);
+        atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + at), (nib ^ nibt) << st);
+        occ = bop3<0xBA>(occ, 1ull << (m & 63), 1ull << ((m >> 6) & 63));
+        stm ^= 1;
+      }
+      nval += (m != 0xFFFFu);
+    };
+    // accepted moves are counted from the ballot words (one popcount pair per
+    // lane per 64 plies) instead of per ply and lane
+    auto flush = [&](u32 base, u32 n) {
+      if (lane < n) {
+        const u64 word = (((u64)bw_hi << 32) | bw_lo) & amask;
+        nacc += (u32)__popcll(word);
+        if (bitmap) bitmap[(size_t)(base + lane) * words + c] = word;
+      }
+    };
+    u32 ply = 0;
+    for (; ply + kReplayPrefetch <= n_plies; ply += kReplayPrefetch) {
+      const u32 s0 = ply & 63;
+#pragma unroll
+      for (int k = 0; k < kReplayPrefetch; ++k) {
+        const u32 m = buf[k];
+        buf[k] = load_move(ply + kReplayPrefetch + k);
+        ply_step(m, s0 + k);
+      }
+      if (((ply + kReplayPrefetch) & 63) == 0) flush(ply + kReplayPrefetch - 64, 64);
+    }
+#pragma unroll
+    for (int k = 0; k < kReplayPrefetch - 1; ++k)
+      if (ply + k < n_plies) ply_step(buf[k], (ply + k) & 63);
+    if ((n_plies & 63) != 0) flush(n_plies & ~63u, n_plies & 63);
+    accepted += nacc;  // a wave-level count: only the block sum is used
+    if (active) {
+      validated += nval;
+      Board b{0, 0, 0, 0};
+#pragma unroll
+      for (u32 j = 0; j < 8; ++j) {
+        const u32 d = my[j * kR3Threads];
+        b.b0 |= (u64)gather_nibble_bits(d) << (8 * j);
+        b.b1 |= (u64)gather_nibble_bits(d >> 1) << (8 * j);
+        b.b2 |= (u64)gather_nibble_bits(d >> 2) << (8 * j);
+        b.b3 |= (u64)gather_nibble_bits(d >> 3) << (8 * j);
+      }
+      const u64 dg = board_digest(b, stm);
+      if (digests) digests[g] = dg;
+      dsum += dg;
+      dxor ^= dg;
+    }
+  }
+  const u64 sv = wave_sum64(validated), sa = wave_sum64(accepted), sd = wave_sum64(dsum);
+  u64 xx = dxor;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) xx ^= __shfl_xor(xx, o, 64);
+  __syncthreads();
+  u64* ws = btw;
+  const u32 w = tid >> 6;
+  if (lane == 0) {
+    ws[w * 4 + 0] = sv;
+    ws[w * 4 + 1] = sa;
+    ws[w * 4 + 2] = sd;
+    ws[w * 4 + 3] = xx;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    u64 r[5] = {0, 0, 0, 0, 0};
+    for (u32 k = 0; k < kR3Threads / 64; ++k) {
+      r[0] += ws[k * 4 + 0];
+      r[1] += ws[k * 4 + 1];
+      r[3] += ws[k * 4 + 2];
+      r[4] ^= ws[k * 4 + 3];
+    }
+    r[2] = r[0] - r[1];
+    for (int k = 0; k < 5; ++k) partial[(size_t)blockIdx.x * 5 + k] = r[k];
+  }
+}
+
 // --------------------------------------------------------------- generator
 // k-th accepted move in (from, to) order: own pieces by ascending square, each
 // piece's targets ascending.
@@ -646,8 +805,17 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
   // n_plies == 0 (no moves buffer to clamp loads into) takes k_replay_ref
   if (n_plies > 0 && !replay_arith()) {
     const u32 nb = replay3_grid(n_games);
-    hipLaunchKernelGGL(k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start),
-                       start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap, digests, partial);
+    // k_replay_ref4 addresses the whole move array through one buffer
+    // descriptor (32-bit offsets); larger batches, and DC_REPLAY=3 in the A/B
+    // build, take k_replay_ref3's per-row descriptors
+    static const bool force3 = [] {
+      const char* e = ab_env("DC_REPLAY");
+      return e && e[0] == '3';
+    }();
+    const bool fits = (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull;
+    hipLaunchKernelGGL((fits && !force3) ? k_replay_ref4 : k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st,
+                       host_mailbox(start), start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap,
+                       digests, partial);
     hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats);
     return hipGetLastError();
   }

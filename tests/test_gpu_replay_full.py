@@ -27,7 +27,7 @@ def sha(a):
 
 def test_replay_10m_bit_exact_vs_golden(engine):
     """The north star's target: all 10M games x 80 plies -- generated on the
-    device, replayed by k_replay_ref3 -- give the golden moves, accept bitmap,
+    device, replayed by k_replay_ref4 -- give the golden moves, accept bitmap,
     per-game digests and counters bit for bit."""
     g = GOLD["c4"]
     n, plies = g["n_games"], GOLD["n_plies"]

@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 export DCHESS_LIB=$PWD/distributed-chess_amd/libdchess_ab.so
 [ -f "$DCHESS_LIB" ] || { echo "build libdchess_ab.so first (make -C distributed-chess_amd ab)"; exit 3; }
 O=gpurun_out; mkdir -p $O
-CNT="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU"
+CNT=${CNT:-"SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU"}
 for p in ${PHASES:-0 1 2 5 6}; do
   DC_C2C_PHASE=$p RUNS=3 timeout -s KILL 90 rocprofv3 --pmc $CNT --output-format csv -d $O/abpmc_$p -o p -- python tools/time_final.py > $O/abpmc_$p.txt 2> $O/abpmc_err.log || { tail -20 $O/abpmc_err.log; exit 2; }
 done

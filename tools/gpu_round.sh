@@ -46,7 +46,7 @@ if has pmc; then
   D8=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d8']['total'])")
   python tools/pmc_summary.py $O --json $O/pmc_latest.json --source "rocprofv3 --pmc (4 passes), bench.py $P" \
     --units "final_d7=k_count2c<=3282734510" --units "dfs_d8=k_perft_dfs<=$D8" \
-    --units "replay=k_replay_ref3=799999953" --units "gen_games=k_gen_games_ref=799999953" \
+    --units "replay=k_replay_ref4=799999953" --units "gen_games=k_gen_games_ref=799999953" \
     --units "state_hash=k_state_hash_ref=1000000" --units "verify_tx=k_verify_tx=262144" > $O/pmc_summary.txt
 fi
 if has txpmc; then
