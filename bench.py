@@ -47,8 +47,11 @@ VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
 #   replay (k_replay_ref, 1M games x 80 plies): 218,408,376 x 64 / 79.9M = 175 per validated move
 # achieved = units/s x W, so the judge can recompute it from the reported rates.
 W_COUNT2 = 20.0
-# REF final stage (last two plies): k_count2c (quiet-move shortcut); DC_FINAL=2b selects k_count2b
-FINAL_KERNEL = "k_count2b" if (os.environ.get("DCHESS_LIB") and os.environ.get("DC_FINAL") == "2b") else "k_count2c"
+# REF final stage: k_count3c (the last three plies: the final stage's parents expanded in-kernel,
+# then the two-ply bulk count of k_count2c); A/B build: DC_FUSED3=0 -> k_count2c, DC_FINAL=2b -> k_count2b
+_AB = os.environ.get("DCHESS_LIB")
+FINAL_KERNEL = ("k_count2b" if (_AB and os.environ.get("DC_FINAL") == "2b")
+                else "k_count2c" if (_AB and os.environ.get("DC_FUSED3") == "0") else "k_count3c")
 W_REPLAY = 175.0
 
 
@@ -269,7 +272,7 @@ def profiled_perft(eng, d, args, pos, depth, steps):
         perft_step(eng, d, args, pos, depth)
     d.sync()
     eng.set_profiling(False)
-    return {k: eng.kernel_stats(k) for k in ("expand_top", "expand_count", "scan", "expand_write", "count2")}
+    return {k: eng.kernel_stats(k) for k in ("expand_top", "expand_count", "scan", "expand_write", "level_moves", "count2")}
 
 
 def _pmc(key):
@@ -336,7 +339,7 @@ def replay_roof(kr, n_games):
 
 
 def roofline(ks, depth, world):
-    """Dominant kernel = the REF final stage (k_count2c: the last two plies, ~85 % of a step).
+    """Dominant kernel = the REF final stage (k_count3c: the last three plies, ~90 % of a step).
     traffic = HBM bytes per launch from the PMC passes (2 x FETCH_SIZE + WRITE_SIZE).
     The HBM side: algorithmic bytes = frontier positions x 40 B read per launch."""
     c2 = ks["count2"]
@@ -348,8 +351,13 @@ def roofline(ks, depth, world):
         rec = None  # PMC of another final-stage kernel
     roof = valu_roof(FINAL_KERNEL, rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
     roof.update({"kernel_avg_ms": avg_s * 1e3, "kernel_leaves_per_s": rate})
-    frontier = REF_STARTPOS[depth - 2] / world  # ply depth-2 positions read by one launch (exact at N=1)
-    alg_bytes = frontier * POS_BYTES
+    if FINAL_KERNEL == "k_count3c":
+        # one u32 move word per final-stage parent (ply depth-2) plus its grandparent's board and root
+        # tag (34 B per ply depth-3 node); the parents themselves never touch HBM as boards
+        alg_bytes = REF_STARTPOS[depth - 2] / world * 4 + REF_STARTPOS[depth - 3] / world * 34
+    else:
+        frontier = REF_STARTPOS[depth - 2] / world  # ply depth-2 positions read by one launch (exact at N=1)
+        alg_bytes = frontier * POS_BYTES
     roof["hbm"] = {"algorithmic_bytes_per_launch": alg_bytes, "achieved_GBps": alg_bytes / avg_s / 1e9,
                    "peak_GBps": HBM_PEAK_GBPS, "frac": alg_bytes / avg_s / 1e9 / HBM_PEAK_GBPS}
     return roof

@@ -101,6 +101,7 @@ struct dc_ctx {
   DBuf<Board> root;
   DBuf<uint16_t> root_meta;
   dc::PerftResult* res_host = nullptr;  // pinned
+  u64* replay_host = nullptr;            // pinned: the replay kernel's five counters
   // The last perft launch sequence, captured as a hipGraph (see perft_run).
   struct PerftKey {
     u32 rules, depth, split, shard, n_shards, stm;
@@ -137,6 +138,7 @@ struct dc_ctx {
   std::string hist_text;   // the escaped start history (host side of the H2D copy)
   DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
+  DBuf<u32> move_words;  // k_count3c: the final stage's parents as move words below their grandparents
   // transaction-signature check: staged strings / offsets / actions / turns,
   // and the G table (built on first use)
   DBuf<char> tx_text;
@@ -165,6 +167,7 @@ struct dc_ctx {
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (rgraph) (void)hipGraphExecDestroy(rgraph);
     if (res_host) (void)hipHostFree(res_host);
+    if (replay_host) (void)hipHostFree(replay_host);
     if (root_host) (void)hipHostFree(root_host);
     pos.release();
     verdicts.release();
@@ -180,6 +183,7 @@ struct dc_ctx {
     bitmap.release();
     digests.release();
     stats5.release();
+    move_words.release();
     for (auto& p : pending) {
       (void)hipEventDestroy(p.a);
       (void)hipEventDestroy(p.b);
@@ -539,21 +543,25 @@ static int replay_impl(dc_ctx* c, uint32_t rules, const dc_pos* start, const uin
   if (start) s = *start;
   else dc_startpos(&s);
   if (s.stm > 1) return DC_EINVAL;
+  // stats5 = [5 totals | partials]; the reduction kernel writes all five totals
   HIP_TRY(c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(std::max<u32>(n_games, 1))));
-  HIP_TRY(hipMemsetAsync(c->stats5.p, 0, 5 * sizeof(u64), c->stream));
+  if (!c->replay_host) HIP_TRY(hipHostMalloc((void**)&c->replay_host, 5 * sizeof(u64)));
   u64* partial = c->stats5.p + 5;
   const Board b{s.bb[0], s.bb[1], s.bb[2], s.bb[3]};
+  bool host_written = false;
   HIP_TRY(c->timed("replay", (u64)n_games * n_plies, [&] {
     return rules == DC_RULES_REF
                ? dc::launch_replay_ref(c->stream, b, s.stm, d_moves, n_games, n_plies, d_bitmap, d_digests, c->stats5.p,
-                                       partial)
+                                       partial, c->replay_host, &host_written)
                : dc::launch_replay_fide(c->stream, reinterpret_cast<const DevPos&>(s), d_moves, n_games, n_plies,
                                         d_bitmap, d_digests, c->stats5.p, partial);
   }));
-  u64 h[5];
-  HIP_TRY(hipMemcpyAsync(h, c->stats5.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+  u64 h[5] = {0, 0, 0, 0, 0};
+  if (!host_written && n_games)
+    HIP_TRY(hipMemcpyAsync(h, c->stats5.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
   int r = sync_ctx(c);
   if (r != DC_SUCCESS) return r;
+  if (host_written) std::memcpy(h, c->replay_host, sizeof h);
   if (stats) {
     stats->validated = h[0];
     stats->accepted = h[1];
@@ -910,6 +918,15 @@ int write_root_host(dc_ctx* c, const dc_pos* pos) {
   return DC_SUCCESS;
 }
 
+// DC_FUSED3=0 (A/B build): the last level is written and counted by k_count2c.
+static bool fused3_enabled() {
+  static const bool on = [] {
+    const char* e = dc::ab_env("DC_FUSED3");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Enqueues one perft on the context stream up to (not including) the result
 // copy.  *host_sync is set when a level size had to be read back on the host
 // (exact mode or a level beyond the speculative budget): such a sequence
@@ -1002,12 +1019,41 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     }));
     return DC_SUCCESS;
   };
+  // REF final stage over the last three plies (k_count3c): the level F is
+  // never written; its parents' level is counted and scanned, then expanded
+  // group by group inside the final stage.  Needs a level to expand (L < F)
+  // that is not the shard level.
+  bool fused3 = !fide && Ldfs == 0 && final_plies == 2 && L < F && !(sharded && S == F) && fused3_enabled();
   while (L < F) {
     const int stm = pos->stm ^ (L & 1);
     if (exact) {
       *host_sync = true;
       e = read_range(c, L, &nb);
       if (e != DC_SUCCESS) return e;
+    }
+    if (fused3 && L + 1 == F && (!exact || nb <= dc::kMoveWordNodesMax)) {
+      // one u32 move word per child; in speculative mode a grandparent level
+      // past kMoveWordNodesMax is flagged on the device (exact rerun)
+      u64 cap_f = std::min<u64>(std::min<u64>(nb, dc::kMoveWordNodesMax) * kBranchBound, 0xFFFFFFFFull);
+      e = count_and_scan(stm, exact ? ~0ull : cap_f, 0);
+      if (e != DC_SUCCESS) return e;
+      if (exact) {
+        *host_sync = true;
+        e = read_range(c, L + 1, &cap_f);
+        if (e != DC_SUCCESS) return e;
+        if (cap_f > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
+      }
+      HIP_TRY(c->move_words.ensure(std::max<u64>(cap_f, 1)));
+      HIP_TRY(c->timed("level_moves", 0, [&] {
+        return dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, c->counts.p, c->chunk_base.p,
+                                      c->move_words.p, cap_f, c->rng.p + L + 1, c->res.p);
+      }));
+      c->last_final = "count2";
+      HIP_TRY(c->timed("count2", 0, [&] {
+        return dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L, c->rng.p + L + 1,
+                                  c->move_words.p, c->res.p);
+      }));
+      return DC_SUCCESS;
     }
     // Speculative mode never reads a level size back: the next level gets
     // min(64 x bound, kSpecBudget) of capacity, a level past it is dropped and

@@ -193,21 +193,52 @@ __device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
 
 __device__ __forceinline__ u32 lane_id() { return __lane_id(); }
 
-// Inclusive prefix sum over the 64 lanes of a wave.
+// DPP lane moves (gfx9 encodings: row_shr:n = 0x110 + n, row_bcast:15 =
+// 0x142, row_bcast:31 = 0x143).  Lanes whose source is outside the row, and
+// lanes of rows masked off by ROWM, read 0.  Scans and reductions built from
+// these stay in the VALU: __shfl_up / __shfl_xor lower to ds_bpermute_b32,
+// an LDS round trip per step that the profiles counted as LDS traffic and
+// bank-conflict cycles (k_count2c's block scans, round 2).
+template <int CTRL, int ROWM = 0xF>
+__device__ __forceinline__ u32 dpp_z(u32 v) {
+  return (u32)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, 0xF, true);
+}
+
+// Inclusive prefix sum over the 64 lanes of a wave: Hillis-Steele inside each
+// 16-lane row (row_shr 1, 2, 4, 8), then row 0's total into row 1 and row 2's
+// into row 3 (row_bcast:15), then rows 0-1's into rows 2-3 (row_bcast:31).
 __device__ __forceinline__ u32 wave_incl_scan(u32 v) {
-  const int lane = (int)lane_id();
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u32 n = __shfl_up(v, o, 64);
-    if (lane >= o) v += n;
-  }
+  v += dpp_z<0x111>(v);
+  v += dpp_z<0x112>(v);
+  v += dpp_z<0x114>(v);
+  v += dpp_z<0x118>(v);
+  v += dpp_z<0x142, 0xA>(v);
+  v += dpp_z<0x143, 0xC>(v);
   return v;
 }
 
-__device__ __forceinline__ u64 wave_sum64(u64 v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// The same on 64-bit values (both halves moved, one 64-bit add per step).
+__device__ __forceinline__ u64 wave_incl_scan64(u64 v) {
+  auto step = [&](auto mv) {
+    const u64 o = ((u64)mv((u32)(v >> 32)) << 32) | mv((u32)v);
+    v += o;
+  };
+  step([](u32 x) { return dpp_z<0x111>(x); });
+  step([](u32 x) { return dpp_z<0x112>(x); });
+  step([](u32 x) { return dpp_z<0x114>(x); });
+  step([](u32 x) { return dpp_z<0x118>(x); });
+  step([](u32 x) { return dpp_z<0x142, 0xA>(x); });
+  step([](u32 x) { return dpp_z<0x143, 0xC>(x); });
   return v;
 }
+
+// Wave-uniform value of lane `l` (l uniform).
+__device__ __forceinline__ u32 lane_bcast(u32 v, u32 l) { return (u32)__builtin_amdgcn_readlane((int)v, (int)l); }
+__device__ __forceinline__ u64 lane_bcast64(u64 v, u32 l) {
+  return ((u64)lane_bcast((u32)(v >> 32), l) << 32) | lane_bcast((u32)v, l);
+}
+
+// Sum over the wave's 64 lanes, wave-uniform (every lane active).
+__device__ __forceinline__ u64 wave_sum64(u64 v) { return lane_bcast64(wave_incl_scan64(v), 63); }
 
 }  // namespace dc

@@ -33,7 +33,7 @@ __device__ __forceinline__ void accumulate_by_tag(u64* divide, u32 tag, u64 v, b
   const u64 vmask = ballot(valid);
   if (vmask == 0) return;
   const int leader = lsb(vmask);
-  const u32 tag0 = __shfl(tag, leader, 64);
+  const u32 tag0 = lane_bcast(tag, (u32)leader);
   const bool same = !valid || tag == tag0;
   if (ballot(same) == ~0ull) {
     const u64 s = wave_sum64(valid ? v : 0);
@@ -58,7 +58,7 @@ __device__ __forceinline__ void tag_hist_add(u64* hist, u32 tag, u64 v, bool val
   const u64 lmask = ballot(live);
   if (lmask == 0) return;
   const int leader = lsb(lmask);
-  const u32 tag0 = __shfl(tag, leader, 64);
+  const u32 tag0 = lane_bcast(tag, (u32)leader);
   if (ballot(live && tag != tag0) == 0) {
     const u64 s = wave_sum64(live ? v : 0);
     if ((int)lane_id() == leader) atomicAdd((unsigned long long*)&hist[tag0], (unsigned long long)s);

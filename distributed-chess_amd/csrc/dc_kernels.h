@@ -55,10 +55,13 @@ hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t
 hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
                             uint8_t* info);
 // stats[5] = validated, accepted, rejected, digest sum, digest xor; partial has
-// replay_partials(n_games) x 5 u64 of scratch.
+// replay_partials(n_games) x 5 u64 of scratch.  *host_written: the five
+// counters were also stored into pinned `stats_host` (valid once the stream is
+// synchronised; no copy needed).
 u32 replay_partials(u32 n_games);
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
-                             u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial);
+                             u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial, u64* stats_host,
+                             bool* host_written);
 hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
                                 uint16_t* out);
 }  // namespace dc

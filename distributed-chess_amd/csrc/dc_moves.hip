@@ -82,7 +82,13 @@ __device__ __forceinline__ void block_stats(u32 validated, u32 accepted, u64 d, 
   }
 }
 
-__global__ __launch_bounds__(256) void k_reduce_stats(const u64* __restrict__ partial, u32 n_blocks, u64* __restrict__ stats) {
+// stats_host (pinned, may be null): the same five counters stored straight
+// into host memory, so a synchronous replay call needs no memset and no copy
+// (they cost ~38 us of a ~0.9 ms call, round 2).  Folding this reduction into
+// the replay kernel's last block instead needed an agent-scope release per
+// block (an L2 writeback on gfx950): 0.86 -> 1.0 ms.
+__global__ __launch_bounds__(256) void k_reduce_stats(const u64* __restrict__ partial, u32 n_blocks, u64* __restrict__ stats,
+                                                      u64* __restrict__ stats_host = nullptr) {
   __shared__ u64 ws[4][5];
   u64 r[5] = {0, 0, 0, 0, 0};
   for (u32 b = threadIdx.x; b < n_blocks; b += blockDim.x) {
@@ -104,6 +110,7 @@ __global__ __launch_bounds__(256) void k_reduce_stats(const u64* __restrict__ pa
       u64 v = ws[0][k];
       for (int w = 1; w < 4; ++w) v = (k == 4) ? (v ^ ws[w][k]) : (v + ws[w][k]);
       stats[k] = v;
+      if (stats_host) __hip_atomic_store(stats_host + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -380,7 +387,12 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref3(Mailbox mb0, u64 occ
 //   - inactive lanes (the last chunk only) replay game n-1 unmasked: their
 //     counters are dropped per chunk and their bitmap bits masked at the
 //     64-ply store, so no per-ply select;
-//   - both ballot halves go into the lanes' words under one M0 write.
+//   - both ballot halves go into the lanes' words under one M0 write;
+//   - LOOK = 1: the two table reads (btw, geo) of ply p + 1 issue before ply
+//     p's mailbox reads, so only the (conflict-free) mailbox round trip is on
+//     a ply's dependency chain; the random, bank-conflicted table gathers
+//     overlap the previous ply's logic.
+template <int LOOK, int PF, bool DW>
 __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ0, u32 stm0, const uint16_t* __restrict__ moves,
                                                            u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
                                                            u64* __restrict__ digests, u64* __restrict__ partial) {
@@ -409,39 +421,67 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
     const bool active = g < n_games;
     const u64 amask = ballot(active);
     const u32 goff = (active ? g : n_games - 1) * 2;
+    // DW (even n_games: every row dword-aligned): the lane loads the dword
+    // holding its move and its neighbour's and rotates its own into the low
+    // half where it is used.  A u16 load is zero-extended by the compiler
+    // right after the load, i.e. at the loop's back edge, where that forces
+    // s_waitcnt vmcnt(0) on all PF prefetched moves, the youngest issued one
+    // ply earlier.  Every use of m reads only its low 16 bits (12-bit
+    // indices, 16-bit compares), so the neighbour's half is harmless.
+    const u32 rot = DW ? (goff & 2u) << 3 : 0u;
     auto load_move = [&](u32 p) -> u32 {
-      return __builtin_amdgcn_raw_buffer_load_b16(rs, goff, min(p, last) * row_bytes, 0);
+      const u32 so = min(p, last) * row_bytes;
+      if constexpr (DW) return __builtin_amdgcn_raw_buffer_load_b32(rs, goff & ~3u, so, 0);
+      else return __builtin_amdgcn_raw_buffer_load_b16(rs, goff, so, 0);
     };
+    auto move_of = [&](u32 d) -> u32 { return DW ? __builtin_amdgcn_alignbit(d, d, rot) : d; };
 #pragma unroll
     for (u32 j = 0; j < 8; ++j) my[j * kR3Threads] = mb0.d[j];
     u64 occ = occ0;
     u32 stm = stm0;
-    u32 nval = 0, nacc = 0;
-    u32 buf[kReplayPrefetch];
+    u32 nvalw = 0, nacc = 0;
+    u32 buf[PF];
 #pragma unroll
-    for (int k = 0; k < kReplayPrefetch; ++k) buf[k] = load_move((u32)k);
+    for (int k = 0; k < PF; ++k) buf[k] = load_move((u32)k);
     u32 bw_lo = 0, bw_hi = 0;  // lane j holds the ballot word of ply 64q + j
-    auto ply_step = [&](u32 m, u32 slot) {
+    struct Tab {
+      u64 bt;
+      u32 gw;
+    };
+    auto tab = [&](u32 m) {
+      return Tab{*reinterpret_cast<const u64*>(r4_smem + ((m << 3) & 0x7FF8u)),
+                 *reinterpret_cast<const u32*>(r4_smem + 4096 * 8 + ((m << 2) & 0x3FFCu))};
+    };
+    // LOOK: `nx` holds ply p's tables on entry and ply p + 1's (move mnext) on
+    // exit; their reads issue after ply p's mailbox reads, which LDS returns
+    // first (in order), so the wait for the mailbox never waits on them
+    Tab nx{0, 0};
+    auto ply_step = [&](u32 m, u32 slot, u32 mnext) {
       const u32 m2 = m << 2, m3 = m << 3;
       const u32 af = __builtin_amdgcn_bitop3_b32(m << 9, tid4, 0x7000u, 0xE4);
       const u32 at = __builtin_amdgcn_bitop3_b32(m3, tid4, 0x7000u, 0xE4);
-      const u64 bt = *reinterpret_cast<const u64*>(r4_smem + (m3 & 0x7FF8u));
-      const u32 gw = *reinterpret_cast<const u32*>(r4_smem + 4096 * 8 + (m2 & 0x3FFCu));
+      const Tab t0 = LOOK ? nx : tab(m);
       const u32 wf = *reinterpret_cast<const u32*>(r4_smem + kR3TabBytes + af);
       const u32 wt = *reinterpret_cast<const u32*>(r4_smem + kR3TabBytes + at);
+      if (LOOK) nx = tab(mnext);
+      const u64 bt = t0.bt;
+      const u32 gw = t0.gw;
       const u32 st = (m >> 4) & 28;
       const u32 nib = __builtin_amdgcn_ubfe(wf, m2, 4);
       const u32 nibt = __builtin_amdgcn_ubfe(wt, st, 4);
       const u32 x = nibt ^ stm;
       const u32 shift = nib | (__builtin_amdgcn_ubfe(kEnemyLut, x, 1) << 4);
       const u32 geo_ok = __builtin_amdgcn_ubfe(gw, shift, 1), own = __builtin_amdgcn_ubfe(kOwnLut, x, 1);
-      const u32 okb = __builtin_amdgcn_bitop3_b32(geo_ok, own, __builtin_amdgcn_bitop3_b32(nib, stm, m >> 15, 0xBE), 0x10);
+      const u32 okb = __builtin_amdgcn_bitop3_b32(geo_ok, own, nib ^ stm, 0x10);  // a & ~b & ~c: only bit 0
       // okb has only bit 0; blocked != 0 iff a square between f and t is
       // occupied, so ok = blocked < okb is one compare (the btw read issues
-      // with the other three for every lane)
+      // with the other three for every lane).  OOR (bit 15) and the sentinel
+      // are 16-bit compares whose masks combine in SALU; every other use of m
+      // reads only its low 12 bits, so the u16 load needs no zero-extension.
       const u32 blocked = __builtin_amdgcn_bitop3_b32((u32)bt, (u32)occ, (u32)(bt >> 32) & (u32)(occ >> 32), 0xEA);  // (a & b) | c
-      const bool ok = blocked < okb;
-      const u64 w = ballot(ok);
+      const bool geo_pass = blocked < okb, in_range = (uint16_t)m < 0x8000u;
+      const bool ok = geo_pass & in_range;
+      const u64 w = ballot(geo_pass) & ballot(in_range);  // two compare masks, one s_and (ballot(ok) rematerialises)
       // the lanes' ballot words are written before the make-move branch, so the
       // compare's own mask feeds both (no mask rematerialised after the branch)
       asm volatile("s_mov_b32 m0, %4\n\tv_writelane_b32 %0, %2, m0\n\tv_writelane_b32 %1, %3, m0"
@@ -454,7 +494,7 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
         occ = bop3<0xBA>(occ, 1ull << (m & 63), 1ull << ((m >> 6) & 63));
         stm ^= 1;
       }
-      nval += (m != 0xFFFFu);
+      nvalw += (u32)__popcll(ballot((uint16_t)m != 0xFFFFu) & amask);  // wave-uniform (SALU)
     };
     // accepted moves are counted from the ballot words (one popcount pair per
     // lane per 64 plies) instead of per ply and lane
@@ -466,23 +506,24 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
       }
     };
     u32 ply = 0;
-    for (; ply + kReplayPrefetch <= n_plies; ply += kReplayPrefetch) {
+    if (LOOK) nx = tab(move_of(buf[0]));
+    for (; ply + PF <= n_plies; ply += PF) {
       const u32 s0 = ply & 63;
 #pragma unroll
-      for (int k = 0; k < kReplayPrefetch; ++k) {
-        const u32 m = buf[k];
-        buf[k] = load_move(ply + kReplayPrefetch + k);
-        ply_step(m, s0 + k);
+      for (int k = 0; k < PF; ++k) {
+        const u32 m = move_of(buf[k]);
+        buf[k] = load_move(ply + PF + k);
+        ply_step(m, s0 + k, LOOK ? move_of(buf[(k + 1) % PF]) : 0u);  // k = PF - 1: ply + PF, reloaded at k = 0
       }
-      if (((ply + kReplayPrefetch) & 63) == 0) flush(ply + kReplayPrefetch - 64, 64);
+      if (((ply + PF) & 63) == 0) flush(ply + PF - 64, 64);
     }
 #pragma unroll
-    for (int k = 0; k < kReplayPrefetch - 1; ++k)
-      if (ply + k < n_plies) ply_step(buf[k], (ply + k) & 63);
+    for (int k = 0; k < PF - 1; ++k)
+      if (ply + k < n_plies) ply_step(move_of(buf[k]), (ply + k) & 63, LOOK ? move_of(buf[k + 1]) : 0u);
     if ((n_plies & 63) != 0) flush(n_plies & ~63u, n_plies & 63);
     accepted += nacc;  // a wave-level count: only the block sum is used
+    if (lane == 0) validated += nvalw;  // wave-level count, added once per wave
     if (active) {
-      validated += nval;
       Board b{0, 0, 0, 0};
 #pragma unroll
       for (u32 j = 0; j < 8; ++j) {
@@ -800,7 +841,9 @@ static Mailbox host_mailbox(const Board& b) {
 }
 
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
-                             u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial) {
+                             u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial, u64* stats_host,
+                             bool* host_written) {
+  *host_written = false;
   if (n_games == 0) return hipSuccess;
   // n_plies == 0 (no moves buffer to clamp loads into) takes k_replay_ref
   if (n_plies > 0 && !replay_arith()) {
@@ -812,17 +855,29 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
       const char* e = ab_env("DC_REPLAY");
       return e && e[0] == '3';
     }();
+    // A/B: DC_REPLAY=41 -> with the table lookahead, =42 -> u16 move loads,
+    // =48 -> 8-ply move prefetch (round 2: 0.98 vs 0.88 ms for 4 plies)
+    static const int v4 = [] {
+      const char* e = ab_env("DC_REPLAY");
+      return (e && e[0] == '4') ? atoi(e) : 0;
+    }();
+    const bool dw = (n_games & 1) == 0 && v4 != 42;
+    auto k4 = dw ? k_replay_ref4<0, 4, true> : k_replay_ref4<0, 4, false>;
+    if (v4 == 41) k4 = dw ? k_replay_ref4<1, 4, true> : k_replay_ref4<1, 4, false>;
+    if (v4 == 48) k4 = dw ? k_replay_ref4<0, 8, true> : k_replay_ref4<0, 8, false>;
     const bool fits = (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull;
-    hipLaunchKernelGGL((fits && !force3) ? k_replay_ref4 : k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st,
+    hipLaunchKernelGGL((fits && !force3) ? k4 : k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st,
                        host_mailbox(start), start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap,
                        digests, partial);
-    hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats);
+    hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats, stats_host);
+    *host_written = stats_host != nullptr;
     return hipGetLastError();
   }
   const u32 nb = blocks_for(n_games, 256);
   hipLaunchKernelGGL(k_replay_ref, dim3(nb), dim3(256), 0, st, start, stm0, moves, n_games, n_plies, bitmap, digests,
                      partial);
-  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats);
+  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats, stats_host);
+  *host_written = stats_host != nullptr;
   return hipGetLastError();
 }
 

@@ -56,6 +56,21 @@ hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* 
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
                         const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res);
 
+// REF, the last three plies without materialising the final stage's parents:
+// after launch_level_count + launch_chunk_scan on the grandparent level `rng`
+// (next Range = rng_ch = [0, children)), k_level_moves writes every child as a
+// u32 move word {grandparent index << 12 | f | t << 6} (mw: children u32),
+// then k_count3c counts plies +2 and +3 below every child.  A grandparent
+// level of more than kMoveWordNodesMax nodes is flagged as overflow (exact
+// rerun).  stm = side to move at the grandparents; res->next_chunk is the
+// group counter.
+constexpr u64 kMoveWordNodesMax = 1ull << 20;
+hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
+                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap, Range* rng_ch,
+                              PerftResult* res);
+hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
+                          const Range* rng_ch, const u32* mw, PerftResult* res);
+
 // K4 (REF): per-lane DFS over L plies below the frontier level `rng` (1 <= L <= 3),
 // each level-L node bulk-counted over the last two plies (perft depth = frontier
 // ply + L + 2).  stm_parent = side to move at the level-L nodes.  stack_frames

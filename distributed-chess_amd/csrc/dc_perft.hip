@@ -80,12 +80,7 @@ __device__ __forceinline__ u32 count_rt(const Board& b, u32 meta, u32 stm) {
 template <int NW>
 __device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* wsum /*LDS[NW]*/, u64* total) {
   const u32 lane = lane_id(), w = threadIdx.x >> 6;
-  u64 incl = v;
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const u64 y = __shfl_up(incl, o, 64);
-    if ((int)lane >= o) incl += y;
-  }
+  const u64 incl = wave_incl_scan64(v);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
   u64 before = 0, all = 0;
@@ -347,12 +342,15 @@ struct WriteShared {
   uint16_t ptag[256];
 };
 
-template <class R, int STM>
+// MW (REF, k_count3c's input): instead of the child's board and tag, its move
+// word {parent index relative to the level << 12 | f | t << 6} goes to
+// mw[chunk_base + slot] (4 instead of 34 bytes per child, same coalescing).
+template <class R, int STM, bool MW = false>
 __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                         const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                         const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
                                                         Board* __restrict__ out, uint16_t* __restrict__ out_meta,
-                                                        uint16_t* __restrict__ out_tags, u64 cap) {
+                                                        uint16_t* __restrict__ out_tags, u64 cap, u32* __restrict__ mw = nullptr) {
   __shared__ WriteShared sh;
   const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
@@ -377,9 +375,11 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
     if (valid) {
       p = load_board(nodes, i);
       pm = load_meta<R>(meta, i);
-      sh.par[tid] = p;
-      if constexpr (R::kMeta) sh.pmeta[tid] = pm;
-      sh.ptag[tid] = tags[i];
+      if constexpr (!MW) {
+        sh.par[tid] = p;
+        if constexpr (R::kMeta) sh.pmeta[tid] = pm;
+        sh.ptag[tid] = tags[i];
+      }
     }
     for (u32 wb = 0; wb < total; wb += kWriteCap) {
       if (wb) __syncthreads();  // previous window fully consumed
@@ -400,6 +400,10 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
         if (o >= cap) continue;
         const u32 e = sh.slot[r];
         const u32 pl = e >> 15;
+        if constexpr (MW) {
+          mw[o] = ((u32)(c * kChunk + pl) << 12) | (e & 0xFFFu);
+          continue;
+        }
         Board ch = sh.par[pl];
         const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
                                              (int)((e >> 12) & 7));
@@ -916,6 +920,65 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
 #endif
 }
 
+// ---------------------------------------- k_count3c (REF: the last three plies)
+// k_count2c fed by its parents' parents: the level above the final stage's
+// parents (perft(7): ply 4, 197k nodes) is counted and scanned as before
+// (k_level_count, k_chunk_scan), but its children (ply 5, 4.9M nodes) are
+// never written as boards.  k_level_moves writes each child as one 32-bit
+// word {grandparent index << 12 | f | t << 6} at its scan offset (20 MB
+// instead of k_level_write's 167 MB of boards and tags), and k_count3c takes
+// groups of 256 consecutive words from a counter: each lane loads its word
+// and its grandparent (a handful of distinct boards per group, L2 hits),
+// makes the child and hands the 256 children to c2c_group.  Every child is
+// counted exactly once and carries its grandparent's root tag.
+// (Round 2: expanding the grandparents inside k_count3c instead -- one lane
+// per grandparent enumerating into LDS while the block waited -- made the
+// final stage 0.56 vs 0.49 + 0.04 ms.)
+constexpr u32 kGroup = 256;
+constexpr u32 kMoveWordNodes = 1u << 20;  // grandparent index field of a move word
+
+// A level of more than kMoveWordNodes grandparents (possible only past a
+// speculative bound) empties the children's Range and flags overflow before
+// the move words are written: the host reruns in exact mode, which takes the
+// k_level_write path.
+__global__ void k_move_word_guard(const Range* __restrict__ rng, Range* __restrict__ rng_ch, PerftResult* __restrict__ res) {
+  if (rng->hi - rng->lo > kMoveWordNodes) {
+    res->overflow = 1;
+    *rng_ch = Range{0, 0};
+  }
+}
+
+template <int STM_G, u32 CAP, int MINW = 4>
+__global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
+                                                 const Range* __restrict__ rng, const Range* __restrict__ rng_ch,
+                                                 const u32* __restrict__ mw, u64* __restrict__ divide,
+                                                 u32* __restrict__ next_group) {
+  __shared__ C2cShared<CAP> sh;
+  tag_hist_init(sh.hist);
+  const u32 tid = threadIdx.x;
+  const u64 lo = rng->lo;
+  const u32 total = (u32)(rng_ch->hi - rng_ch->lo);  // children (< 2^32: launcher)
+  for (;;) {
+    if (tid == 0) sh.next = atomicAdd(next_group, 1u);
+    __syncthreads();
+    const u64 s = (u64)sh.next * kGroup;
+    if (s >= total) break;  // block-uniform
+    const u64 i = s + tid;
+    const bool valid = i < total;
+    Board ch{0, 0, 0, 0};
+    u32 tag = 0;
+    if (valid) {
+      const u32 e = mw[i];
+      const u64 g = lo + (e >> 12);
+      ch = load_board(nodes, g);
+      tag = tags[g];
+      ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
+    }
+    c2c_group<1 - STM_G, CAP>(sh, valid, ch, tag, divide);
+  }
+  tag_hist_flush(sh.hist, divide);
+}
+
 // ------------------------------------------------- K4: per-lane DFS (REF)
 // perft below a frontier level without materialising the deeper levels: every
 // lane walks the subtree of one frontier node depth first with an explicit
@@ -1110,7 +1173,7 @@ hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* n
                               const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
                               const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap) {
   DC_LAUNCH_RULES_STM(k_level_write, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, counts, chunk_base,
-                      out, out_meta, out_tags, cap);
+                      out, out_meta, out_tags, cap, (u32*)nullptr);
   return hipGetLastError();
 }
 
@@ -1253,6 +1316,32 @@ hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* 
     return hipErrorNotSupported;
   }
 #undef DC_DFS
+  return hipGetLastError();
+}
+
+hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
+                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap, Range* rng_ch,
+                              PerftResult* res) {
+  hipLaunchKernelGGL(k_move_word_guard, dim3(1), dim3(1), 0, st, rng, rng_ch, res);
+  // words beyond mw_cap are dropped (a flagged level is never read)
+  auto k = stm ? k_level_write<RefRules, 1, true> : k_level_write<RefRules, 0, true>;
+  hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, grid_for(std::min<u64>(n_bound, kMoveWordNodes), kChunk))),
+                     dim3(256), 0, st, nodes, nullptr, nullptr, rng, counts, chunk_base, nullptr, nullptr, nullptr,
+                     mw_cap, mw);
+  return hipGetLastError();
+}
+
+hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
+                          const Range* rng_ch, const u32* mw, PerftResult* res) {
+  if (stm_g) {
+    auto k = k_count3c<1, 256 * 24>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
+                       res->divide, &res->next_chunk);
+  } else {
+    auto k = k_count3c<0, 256 * 24>;
+    hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
+                       res->divide, &res->next_chunk);
+  }
   return hipGetLastError();
 }
 

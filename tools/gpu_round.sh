@@ -45,7 +45,7 @@ if has pmc; then
   pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" p4 || { tail $O/pmc.err; exit 5; }
   D8=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d8']['total'])")
   python tools/pmc_summary.py $O --json $O/pmc_latest.json --source "rocprofv3 --pmc (4 passes), bench.py $P" \
-    --units "final_d7=k_count2c<=3282734510" --units "dfs_d8=k_perft_dfs<=$D8" \
+    --units "final_d7=k_count3c<=3282734510" --units "dfs_d8=k_perft_dfs<=$D8" \
     --units "replay=k_replay_ref4=799999953" --units "gen_games=k_gen_games_ref=799999953" \
     --units "state_hash=k_state_hash_ref=1000000" --units "verify_tx=k_verify_tx=262144" > $O/pmc_summary.txt
 fi
