@@ -302,17 +302,20 @@ def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
     measured = w is not None
     w = w if measured else w_frozen
     peak = VALU_PEAK_LANE_OPS
+    # without a PMC record of THIS kernel there is no W: frozen W (an upper bound
+    # on the work of the first parity kernel) would overstate the fraction
     roof = {"bound": "valu", "kernel": kernel, "unit": "TOPS (int32 VALU lane-ops/s)",
-            "achieved": rate * w / 1e12, "peak": peak / 1e12, "frac": rate * w / peak,
+            "achieved": rate * w / 1e12 if measured else None, "peak": peak / 1e12,
+            "frac": rate * w / peak if measured else None,
             f"W_lane_ops_per_{unit_name}": w,
             "W_source": pmc_rec["source"] if measured else "frozen (no PMC record for this kernel)",
             f"W_frozen_per_{unit_name}": w_frozen,
-            "algorithmic_gain_vs_frozen_W": w_frozen / w if (w and w_frozen) else None,
+            "algorithmic_gain_vs_frozen_W": w_frozen / w if (measured and w_frozen) else None,
             "traffic": pmc_rec.get("hbm_bytes_per_launch") if pmc_rec else None}
     if pmc_rec:
         util = pmc_rec.get("valu_utilization")
         w_int = pmc_rec.get("int_lane_ops_per_unit")
-        if util is not None:
+        if util is not None and measured:
             roof["valu_utilization"] = util
             roof["frac_active_lanes"] = roof["frac"] * util
         if w_int is not None:
