@@ -100,6 +100,7 @@ struct dc_ctx {
   DBuf<u64> dfs_stack;  // K4 frames (dc_perft.hip k_perft_dfs)
   DBuf<Board> root;
   DBuf<uint16_t> root_meta;
+  DBuf<dc::ResultCursor> rcur;  // dc_perft_repeat_device: where the next run's result goes
   dc::PerftResult* res_host = nullptr;  // pinned
   u64* replay_host = nullptr;            // pinned: the replay kernel's five counters
   // The last perft launch sequence, captured as a hipGraph (see perft_run).
@@ -977,6 +978,21 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
+  // REF final stage over the last three plies (k_count3c): the level F is
+  // never written; its parents' level is counted and scanned, then expanded
+  // group by group inside the final stage.  Needs a level to expand (L < F)
+  // that is not the shard level.
+  const bool fused3 = !fide && Ldfs == 0 && final_plies == 2 && T < F && !(sharded && S == F) && fused3_enabled();
+  // Capacity of level L + 1 (and the node guard of level L) in speculative
+  // mode: the move-word level of the fused final stage, else a board level.
+  auto spec_cap = [&](u32 lvl, u64 n_lvl, u64* guard) -> u64 {
+    if (fused3 && lvl + 1 == F) {
+      *guard = dc::kMoveWordNodesMax;
+      return std::min<u64>(std::min<u64>(n_lvl, dc::kMoveWordNodesMax) * kBranchBound, 0xFFFFFFFFull);
+    }
+    *guard = 0;
+    return std::min(n_lvl * kBranchBound, kSpecBudget / kNodeBytes);
+  };
   // the result block is cleared by k_expand_top itself (its first stores)
   HIP_TRY(c->timed("expand_top", 0, [&] {
     return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, ts, c->nodes[0].p,
@@ -1004,7 +1020,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     if (e != DC_SUCCESS) return e;
   }
   // One level: counts + chunk sums, chunk scan into Range L+1 (capacity cap), then `write`.
-  auto count_and_scan = [&](int stm, u64 cap, int select_path) -> int {
+  auto count_and_scan = [&](int stm, u64 cap, int select_path, u64 guard) -> int {
     const u64 nch = std::max<u64>(dc::chunks_for(nb), 1);
     HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
     HIP_TRY(c->chunk_sum.ensure(nch));
@@ -1015,15 +1031,10 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     }));
     HIP_TRY(c->timed("scan", 0, [&] {
       return dc::launch_chunk_scan(c->stream, c->chunk_sum.p, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, cap,
-                                   c->res.p, select_path);
+                                   c->res.p, select_path, guard);
     }));
     return DC_SUCCESS;
   };
-  // REF final stage over the last three plies (k_count3c): the level F is
-  // never written; its parents' level is counted and scanned, then expanded
-  // group by group inside the final stage.  Needs a level to expand (L < F)
-  // that is not the shard level.
-  bool fused3 = !fide && Ldfs == 0 && final_plies == 2 && L < F && !(sharded && S == F) && fused3_enabled();
   while (L < F) {
     const int stm = pos->stm ^ (L & 1);
     if (exact) {
@@ -1034,8 +1045,9 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     if (fused3 && L + 1 == F && (!exact || nb <= dc::kMoveWordNodesMax)) {
       // one u32 move word per child; in speculative mode a grandparent level
       // past kMoveWordNodesMax is flagged on the device (exact rerun)
-      u64 cap_f = std::min<u64>(std::min<u64>(nb, dc::kMoveWordNodesMax) * kBranchBound, 0xFFFFFFFFull);
-      e = count_and_scan(stm, exact ? ~0ull : cap_f, 0);
+      u64 guard = 0;
+      u64 cap_f = spec_cap(L, nb, &guard);
+      e = count_and_scan(stm, exact ? ~0ull : cap_f, 0, exact ? 0 : guard);
       if (e != DC_SUCCESS) return e;
       if (exact) {
         *host_sync = true;
@@ -1046,7 +1058,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       HIP_TRY(c->move_words.ensure(std::max<u64>(cap_f, 1)));
       HIP_TRY(c->timed("level_moves", 0, [&] {
         return dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, c->counts.p, c->chunk_base.p,
-                                      c->move_words.p, cap_f, c->rng.p + L + 1, c->res.p);
+                                      c->move_words.p, cap_f);
       }));
       c->last_final = "count2";
       HIP_TRY(c->timed("count2", 0, [&] {
@@ -1061,9 +1073,10 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     // kernels use resident grids over device Ranges, so a loose bound costs
     // memory, not launches.  (Reading the ply-4 size back cost perft(7) one
     // host sync mid-run and kept it out of the graph.)
-    u64 cap_next = exact ? nb * kBranchBound : std::min(nb * kBranchBound, kSpecBudget / kNodeBytes);
+    u64 guard_unused = 0;
+    u64 cap_next = exact ? nb * kBranchBound : spec_cap(L, nb, &guard_unused);
     const bool exact_next = exact;
-    e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0);
+    e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0, 0);
     if (e != DC_SUCCESS) return e;
     if (exact_next) {
       *host_sync = true;
@@ -1229,6 +1242,7 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     return DC_EINVAL;
   if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
   if (n_runs == 0) return DC_SUCCESS;
+  HIP_TRY(c->rcur.ensure(1));  // before the key: an allocation moves the epoch
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
   const bool graphable = !c->profiling && perft_graphs_enabled();
   if (!c->root_host || !(graphable && c->rgraph && c->rkey == key)) {
@@ -1240,11 +1254,12 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     if (c->last_exact) {
       // speculative capacities overflow for this configuration: exact runs
       // (one host sync per level), each result still left on the device
+      HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out)));
       for (u32 i = 0; i < n_runs; ++i) {
         bool hs = false;
         e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs);
         if (e != DC_SUCCESS) return e;
-        HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, reinterpret_cast<u64*>(d_out) + (size_t)258 * i));
+        HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
       }
       return DC_SUCCESS;
     }
@@ -1256,7 +1271,9 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
       }
       if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
         bool hs = false;
-        const int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
+        // the result copy is part of the graph: its destination is the cursor
+        int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
+        if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
         hipGraph_t g = nullptr;
         const hipError_t ee = hipStreamEndCapture(c->stream, &g);
         if (ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
@@ -1281,15 +1298,16 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
+  HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out)));
   for (u32 i = 0; i < n_runs; ++i) {
     if (use_graph) {
-      HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));
+      HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
     } else {
       bool host_sync = false;
       int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync);
       if (e != DC_SUCCESS) return e;
+      HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
     }
-    HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, reinterpret_cast<u64*>(d_out) + (size_t)258 * i));
   }
   return DC_SUCCESS;
 }

@@ -37,15 +37,25 @@ hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const
 u64 chunks_for(u64 n);
 hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
                               const Range* rng, u64 n_bound, u32* counts, u64* chunk_sum);
+// guard != 0: a level `rng` of more than guard nodes is flagged as overflow
+// (next = empty), as a total beyond cap is (the move-word path's node limit).
 hipError_t launch_chunk_scan(hipStream_t st, const u64* chunk_sum, const Range* rng, u64* chunk_base, Range* next,
-                             u64 cap, PerftResult* res, int select_path);
+                             u64 cap, PerftResult* res, int select_path, u64 guard = 0);
 hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
                               const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
                               const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap);
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
 // out[0..256) = the run's divide (0 past n_root), out[256] = n_root | overflow << 32,
 // out[257] = the total: one run's result kept on the device (dc_perft_repeat_device).
-hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, u64* out);
+// The destination is read from a device-side cursor {base, run index} that the
+// copy advances, so one captured graph (perft + copy) serves every run:
+// launch_set_result_cursor points it at base, run 0.
+struct ResultCursor {
+  u64* base;
+  u64 idx;
+};
+hipError_t launch_set_result_cursor(hipStream_t st, ResultCursor* cur, u64* base);
+hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, ResultCursor* cur);
 // Strided shard: every n_shards-th node of the level, gathered to out[0..).
 hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* in_meta, const uint16_t* in_tags,
                                Range* rng, u32 shard, u32 n_shards, Board* out, uint16_t* out_meta,
@@ -64,10 +74,11 @@ hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Boa
 // level of more than kMoveWordNodesMax nodes is flagged as overflow (exact
 // rerun).  stm = side to move at the grandparents; res->next_chunk is the
 // group counter.
+// The node limit is checked by the scan that sizes the children (guard =
+// kMoveWordNodesMax in launch_chunk_scan).
 constexpr u64 kMoveWordNodesMax = 1ull << 20;
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
-                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap, Range* rng_ch,
-                              PerftResult* res);
+                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap);
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
                           const Range* rng_ch, const u32* mw, PerftResult* res);
 

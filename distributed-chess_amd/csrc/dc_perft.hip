@@ -300,7 +300,8 @@ __global__ __launch_bounds__(256) void k_level_count(const Board* __restrict__ n
 // (res->path = 1) and leaves the descriptor range empty.
 __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restrict__ chunk_sum, const Range* __restrict__ rng,
                                                              u64* __restrict__ chunk_base, Range* __restrict__ next,
-                                                             u64 cap, PerftResult* __restrict__ res, int select_path) {
+                                                             u64 cap, PerftResult* __restrict__ res, int select_path,
+                                                             u64 guard) {
   __shared__ u64 wsum[kTopThreads / 64];
   const u64 nch = (rng->hi - rng->lo + kChunk - 1) / kChunk;
   const u64 per = (nch + kTopThreads - 1) / kTopThreads;
@@ -317,8 +318,9 @@ __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restric
   if (threadIdx.x == 0) {
     // large parent levels keep count2 busy on their own: no descriptor round trip
     if (select_path && rng->hi - rng->lo > (u64)select_path) total = cap + 1;
-    if (total > cap) {  // the level would not fit: flag it (or pick count2) and leave the range empty
-      if (select_path) res->path = 1;
+    const bool guard_hit = guard && rng->hi - rng->lo > guard;
+    if (total > cap || guard_hit) {  // the level would not fit: flag it (or pick count2) and leave the range empty
+      if (select_path && !guard_hit) res->path = 1;
       else res->overflow = 1;
       *next = Range{0, 0};
     } else {
@@ -938,16 +940,9 @@ constexpr u32 kGroup = 256;
 constexpr u32 kMoveWordNodes = 1u << 20;  // grandparent index field of a move word
 
 // A level of more than kMoveWordNodes grandparents (possible only past a
-// speculative bound) empties the children's Range and flags overflow before
-// the move words are written: the host reruns in exact mode, which takes the
-// k_level_write path.
-__global__ void k_move_word_guard(const Range* __restrict__ rng, Range* __restrict__ rng_ch, PerftResult* __restrict__ res) {
-  if (rng->hi - rng->lo > kMoveWordNodes) {
-    res->overflow = 1;
-    *rng_ch = Range{0, 0};
-  }
-}
-
+// speculative bound) is flagged by the scan that sizes its children
+// (k_chunk_scan's guard): the children's Range is empty and
+// the host reruns in exact mode, which takes the k_level_write path.
 template <int STM_G, u32 CAP, int MINW = 4>
 __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, const Range* __restrict__ rng_ch,
@@ -1163,9 +1158,9 @@ hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* n
 }
 
 hipError_t launch_chunk_scan(hipStream_t st, const u64* chunk_sum, const Range* rng, u64* chunk_base, Range* next,
-                             u64 cap, PerftResult* res, int select_path) {
+                             u64 cap, PerftResult* res, int select_path, u64 guard) {
   hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(kTopThreads), 0, st, chunk_sum, rng, chunk_base, next, cap, res,
-                     select_path);
+                     select_path, guard);
   return hipGetLastError();
 }
 
@@ -1185,8 +1180,17 @@ hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* 
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_copy_result(const PerftResult* __restrict__ r, u64* __restrict__ out) {
+__global__ void k_set_result_cursor(ResultCursor* cur, u64* base) { *cur = ResultCursor{base, 0}; }
+
+hipError_t launch_set_result_cursor(hipStream_t st, ResultCursor* cur, u64* base) {
+  hipLaunchKernelGGL(k_set_result_cursor, dim3(1), dim3(1), 0, st, cur, base);
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_copy_result(const PerftResult* __restrict__ r, ResultCursor* __restrict__ cur) {
   __shared__ u64 ws[4];
+  const ResultCursor rc = *cur;  // every thread reads it before thread 0 advances it
+  u64* __restrict__ out = rc.base + 258 * rc.idx;
   const u32 i = threadIdx.x, nr = r->n_root;
   const u64 v = i < nr ? r->divide[i] : 0;
   out[i] = v;
@@ -1196,11 +1200,12 @@ __global__ __launch_bounds__(256) void k_copy_result(const PerftResult* __restri
   if (i == 0) {
     out[256] = (u64)nr | ((u64)r->overflow << 32);
     out[257] = ws[0] + ws[1] + ws[2] + ws[3];
+    cur->idx = rc.idx + 1;  // after the barrier: all threads hold rc
   }
 }
 
-hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, u64* out) {
-  hipLaunchKernelGGL(k_copy_result, dim3(1), dim3(256), 0, st, res, out);
+hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, ResultCursor* cur) {
+  hipLaunchKernelGGL(k_copy_result, dim3(1), dim3(256), 0, st, res, cur);
   return hipGetLastError();
 }
 
@@ -1320,9 +1325,7 @@ hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* 
 }
 
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
-                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap, Range* rng_ch,
-                              PerftResult* res) {
-  hipLaunchKernelGGL(k_move_word_guard, dim3(1), dim3(1), 0, st, rng, rng_ch, res);
+                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap) {
   // words beyond mw_cap are dropped (a flagged level is never read)
   auto k = stm ? k_level_write<RefRules, 1, true> : k_level_write<RefRules, 0, true>;
   hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, grid_for(std::min<u64>(n_bound, kMoveWordNodes), kChunk))),
