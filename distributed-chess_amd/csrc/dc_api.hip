@@ -92,8 +92,9 @@ struct dc_ctx {
   DBuf<uint16_t> meta[2];  // FIDE castle/ep per node
   DBuf<Board> top_nodes;
   DBuf<uint16_t> top_tags, top_meta;
-  DBuf<u32> counts;
-  DBuf<u64> chunk_sum, chunk_base;
+  DBuf<u32> counts, counts2;        // a level's move counts; counts2: the next level's,
+  DBuf<u64> chunk_sum, chunk_sum2;  // made by the k_level_write that writes it
+  DBuf<u64> chunk_base;
   DBuf<dc::PerftResult> res;
   DBuf<dc::Range> rng;
   DBuf<u64> desc;
@@ -159,7 +160,9 @@ struct dc_ctx {
     for (auto* b : {&nodes[0], &nodes[1], &top_nodes, &root}) b->release();
     for (auto* b : {&tags[0], &tags[1], &meta[0], &meta[1], &top_tags, &top_meta, &root_meta, &moves}) b->release();
     counts.release();
+    counts2.release();
     chunk_sum.release();
+    chunk_sum2.release();
     chunk_base.release();
     res.release();
     rng.release();
@@ -1019,19 +1022,33 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     e = take_shard();
     if (e != DC_SUCCESS) return e;
   }
+  // Level L's counts and chunk sums live in buffer pair cb; the k_level_write
+  // that makes level L + 1 can count it into the other pair (counted: no
+  // k_level_count launch for it).
+  int cb = 0;
+  bool counted = false;
+  DBuf<u32>* cnt_buf[2] = {&c->counts, &c->counts2};
+  DBuf<u64>* sum_buf[2] = {&c->chunk_sum, &c->chunk_sum2};
   // One level: counts + chunk sums, chunk scan into Range L+1 (capacity cap), then `write`.
-  auto count_and_scan = [&](int stm, u64 cap, int select_path, u64 guard) -> int {
+  // count_next: level L + 1 will be counted by the write (its chunk sums are cleared here).
+  auto count_and_scan = [&](int stm, u64 cap, int select_path, u64 guard, bool count_next) -> int {
     const u64 nch = std::max<u64>(dc::chunks_for(nb), 1);
-    HIP_TRY(c->counts.ensure(std::max<u64>(nb, 1)));
-    HIP_TRY(c->chunk_sum.ensure(nch));
+    HIP_TRY(cnt_buf[cb]->ensure(std::max<u64>(nb, 1)));
+    HIP_TRY(sum_buf[cb]->ensure(nch));
     HIP_TRY(c->chunk_base.ensure(nch));
-    HIP_TRY(c->timed("expand_count", 0, [&] {
-      return dc::launch_level_count(c->stream, rules, stm, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
-                                    c->rng.p + L, nb, c->counts.p, c->chunk_sum.p);
-    }));
+    const u64 nch_next = std::max<u64>(dc::chunks_for(std::min<u64>(cap, 0xFFFFFFFFull)), 1);
+    if (count_next) {
+      HIP_TRY(cnt_buf[cb ^ 1]->ensure(std::max<u64>(std::min<u64>(cap, 0xFFFFFFFFull), 1)));
+      HIP_TRY(sum_buf[cb ^ 1]->ensure(nch_next));
+    }
+    if (!counted)
+      HIP_TRY(c->timed("expand_count", 0, [&] {
+        return dc::launch_level_count(c->stream, rules, stm, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
+                                      c->rng.p + L, nb, cnt_buf[cb]->p, sum_buf[cb]->p);
+      }));
     HIP_TRY(c->timed("scan", 0, [&] {
-      return dc::launch_chunk_scan(c->stream, c->chunk_sum.p, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, cap,
-                                   c->res.p, select_path, guard);
+      return dc::launch_chunk_scan(c->stream, sum_buf[cb]->p, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, cap,
+                                   c->res.p, select_path, guard, count_next ? sum_buf[cb ^ 1]->p : nullptr, nch_next);
     }));
     return DC_SUCCESS;
   };
@@ -1047,7 +1064,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       // past kMoveWordNodesMax is flagged on the device (exact rerun)
       u64 guard = 0;
       u64 cap_f = spec_cap(L, nb, &guard);
-      e = count_and_scan(stm, exact ? ~0ull : cap_f, 0, exact ? 0 : guard);
+      e = count_and_scan(stm, exact ? ~0ull : cap_f, 0, exact ? 0 : guard, false);
       if (e != DC_SUCCESS) return e;
       if (exact) {
         *host_sync = true;
@@ -1057,8 +1074,8 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       }
       HIP_TRY(c->move_words.ensure(std::max<u64>(cap_f, 1)));
       HIP_TRY(c->timed("level_moves", 0, [&] {
-        return dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, c->counts.p, c->chunk_base.p,
-                                      c->move_words.p, cap_f);
+        return dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, cnt_buf[cb]->p,
+                                      c->chunk_base.p, c->move_words.p, cap_f);
       }));
       c->last_final = "count2";
       HIP_TRY(c->timed("count2", 0, [&] {
@@ -1076,7 +1093,11 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     u64 guard_unused = 0;
     u64 cap_next = exact ? nb * kBranchBound : spec_cap(L, nb, &guard_unused);
     const bool exact_next = exact;
-    e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0, 0);
+    // the write counts level L + 1 when that level is counted next (not the
+    // final stage's level, not a level first cut to this rank's shard)
+    // (speculative mode only: exact mode sizes the next level after the scan)
+    const bool count_next = !exact && L + 1 < F && !(sharded && L + 1 == S);
+    e = count_and_scan(stm, exact_next ? ~0ull : cap_next, 0, 0, count_next);
     if (e != DC_SUCCESS) return e;
     if (exact_next) {
       *host_sync = true;
@@ -1088,11 +1109,14 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     if (e != DC_SUCCESS) return e;
     HIP_TRY(c->timed("expand_write", 0, [&] {
       return dc::launch_level_write(c->stream, rules, stm, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
-                                    c->tags[buf].p, c->rng.p + L, nb, c->counts.p, c->chunk_base.p,
+                                    c->tags[buf].p, c->rng.p + L, nb, cnt_buf[cb]->p, c->chunk_base.p,
                                     c->nodes[buf ^ 1].p, fide ? c->meta[buf ^ 1].p : nullptr, c->tags[buf ^ 1].p,
-                                    cap_next);
+                                    cap_next, count_next ? cnt_buf[cb ^ 1]->p : nullptr,
+                                    count_next ? sum_buf[cb ^ 1]->p : nullptr);
     }));
     buf ^= 1;
+    counted = count_next;
+    if (count_next) cb ^= 1;
     ++L;
     nb = cap_next;
     if (sharded && L == S) {

@@ -20,8 +20,11 @@
 // k_escape_write, below) from raw UTF-8 resident in HBM; the tokens the kernel
 // appends are plain ASCII.
 //
-// Per lane: pass 1 replays the game to learn the final turn (the first JSON
-// field); pass 2 replays it again and streams the JSON bytes into the sponge.
+// Per lane: pass 1 replays the game (ref_verdict + make per ply) to learn the
+// final turn (the first JSON field) and records each ply's verdict as one bit
+// in LDS (the first kAccPlies plies); pass 2 streams the JSON bytes into the
+// sponge, re-making only the accepted moves from those bits (plies past
+// kAccPlies are validated again).  Round 1 validated every ply twice.
 // Bytes are produced into the lane's 136-byte block in LDS by a small piece
 // state machine (template strings, names, start history, per-move tokens,
 // board cells); every lane emits exactly one block per step, so the
@@ -96,6 +99,7 @@ __device__ __forceinline__ u32 kind_index(u32 code) {
 
 constexpr u32 kHashThreads = 256;
 constexpr u32 kTokBytes = 16;
+constexpr u32 kAccPlies = 128;  // per-lane verdict bits kept from pass 1 (4 dwords of LDS)
 
 // Stages of a lane's JSON stream (in order).
 enum : u32 {
@@ -112,6 +116,7 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   __shared__ char tpl[sizeof(g_json_tpl.s)];
   __shared__ __attribute__((aligned(8))) uint8_t blk[kHashThreads][kKeccakRate];
   __shared__ char tok[kHashThreads][kTokBytes];
+  __shared__ u32 accb[kAccPlies / 32][kHashThreads];  // [word][lane]: bank per lane
   const u32 tid = threadIdx.x;
   for (u32 i = tid; i < sizeof(g_json_tpl.s); i += kHashThreads) tpl[i] = g_json_tpl.s[i];
   __syncthreads();
@@ -121,11 +126,18 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   u32 stm = stm0;
   if (active) {
     Board b = start;
+    u32 bits = 0;
     for (u32 p = 0; p < n_plies; ++p) {
       const u32 m = moves[(size_t)p * n_games + g];
-      if (m != 0xFFFFu && ref_verdict(b, stm, m) == V_OK) {
+      const bool ok = m != 0xFFFFu && ref_verdict(b, stm, m) == V_OK;
+      if (ok) {
         ref_make(b, (int)(m & 63), (int)((m >> 6) & 63));
         stm ^= 1;
+      }
+      bits |= (u32)ok << (p & 31);
+      if ((p & 31) == 31 || p + 1 == n_plies) {
+        if (p < kAccPlies) accb[p >> 5][tid] = bits;
+        bits = 0;
       }
     }
   }
@@ -172,9 +184,10 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           // next accepted move: apply it and write its token "[ ]N. san"
           rem = 0;
           while (ply < n_plies && rem == 0) {
-            const u32 m = moves[(size_t)ply * n_games + g];
-            ++ply;
-            if (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK) continue;
+            const u32 p = ply++;
+            if (p < kAccPlies && ((accb[p >> 5][tid] >> (p & 31)) & 1) == 0) continue;  // rejected in pass 1
+            const u32 m = moves[(size_t)p * n_games + g];
+            if (p >= kAccPlies && (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK)) continue;
             const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
             const u32 ki = kind_index(nibble(b, f) >> 1);
             const bool cap = (occupied(b) >> t) & 1;

@@ -39,11 +39,18 @@ hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* n
                               const Range* rng, u64 n_bound, u32* counts, u64* chunk_sum);
 // guard != 0: a level `rng` of more than guard nodes is flagged as overflow
 // (next = empty), as a total beyond cap is (the move-word path's node limit).
+// zero_next != nullptr: also clears the next level's first chunk sums (at most
+// zero_max), which launch_level_write(next_sum) then accumulates.
 hipError_t launch_chunk_scan(hipStream_t st, const u64* chunk_sum, const Range* rng, u64* chunk_base, Range* next,
-                             u64 cap, PerftResult* res, int select_path, u64 guard = 0);
+                             u64 cap, PerftResult* res, int select_path, u64 guard = 0, u64* zero_next = nullptr,
+                             u64 zero_max = 0);
+// next_counts != nullptr: the children's own move counts (next_counts[i]) and
+// per-chunk sums (added into next_sum, cleared by the chunk scan) are made
+// here, so the next level needs no launch_level_count.
 hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
                               const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
-                              const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap);
+                              const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap,
+                              u32* next_counts = nullptr, u64* next_sum = nullptr);
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
 // out[0..256) = the run's divide (0 past n_root), out[256] = n_root | overflow << 32,
 // out[257] = the total: one run's result kept on the device (dc_perft_repeat_device).

@@ -301,7 +301,7 @@ __global__ __launch_bounds__(256) void k_level_count(const Board* __restrict__ n
 __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restrict__ chunk_sum, const Range* __restrict__ rng,
                                                              u64* __restrict__ chunk_base, Range* __restrict__ next,
                                                              u64 cap, PerftResult* __restrict__ res, int select_path,
-                                                             u64 guard) {
+                                                             u64 guard, u64* __restrict__ zero, u64 zero_max) {
   __shared__ u64 wsum[kTopThreads / 64];
   const u64 nch = (rng->hi - rng->lo + kChunk - 1) / kChunk;
   const u64 per = (nch + kTopThreads - 1) / kTopThreads;
@@ -314,6 +314,12 @@ __global__ __launch_bounds__(kTopThreads) void k_chunk_scan(const u64* __restric
     const u64 v = chunk_sum[c];
     chunk_base[c] = run;
     run += v;
+  }
+  // zero != nullptr: the next level's chunk sums are accumulated by the
+  // k_level_write that makes it (ncounts/nsum): clear its chunks first
+  if (zero) {
+    const u64 nz = min((total + kChunk - 1) / kChunk, zero_max);
+    for (u64 c = threadIdx.x; c < nz; c += kTopThreads) zero[c] = 0;
   }
   if (threadIdx.x == 0) {
     // large parent levels keep count2 busy on their own: no descriptor round trip
@@ -352,7 +358,8 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
                                                         const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                         const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
                                                         Board* __restrict__ out, uint16_t* __restrict__ out_meta,
-                                                        uint16_t* __restrict__ out_tags, u64 cap, u32* __restrict__ mw = nullptr) {
+                                                        uint16_t* __restrict__ out_tags, u64 cap, u32* __restrict__ mw = nullptr,
+                                                        u32* __restrict__ ncounts = nullptr, u64* __restrict__ nsum = nullptr) {
   __shared__ WriteShared sh;
   const u32 tid = threadIdx.x;
   const u64 lo = rng->lo, hi = rng->hi;
@@ -397,21 +404,41 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
         });
       }
       __syncthreads();
-      for (u32 r = tid; r < nslots; r += 256) {
+      // wave-uniform rounds (the children's counts are wave-reduced)
+      for (u32 r0 = 0; r0 < nslots; r0 += 256) {
+        const u32 r = r0 + tid;
         const u64 o = base_out + base + r;
-        if (o >= cap) continue;
-        const u32 e = sh.slot[r];
-        const u32 pl = e >> 15;
-        if constexpr (MW) {
-          mw[o] = ((u32)(c * kChunk + pl) << 12) | (e & 0xFFFu);
-          continue;
+        const bool live = r < nslots && o < cap;
+        u32 cnt = 0;
+        if (live) {
+          const u32 e = sh.slot[r];
+          const u32 pl = e >> 15;
+          if constexpr (MW) {
+            mw[o] = ((u32)(c * kChunk + pl) << 12) | (e & 0xFFFu);
+          } else {
+            Board ch = sh.par[pl];
+            const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
+                                                 (int)((e >> 12) & 7));
+            store_board(out, o, ch);
+            if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
+            out_tags[o] = sh.ptag[pl];
+            // ncounts (the next level is counted here, not by k_level_count):
+            // the child's own move count, added into its 256-node chunk's sum
+            if (ncounts) {
+              cnt = R::template count<1 - STM>(ch, cm);
+              ncounts[o] = cnt;
+            }
+          }
         }
-        Board ch = sh.par[pl];
-        const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
-                                             (int)((e >> 12) & 7));
-        store_board(out, o, ch);
-        if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
-        out_tags[o] = sh.ptag[pl];
+        if (!MW && ncounts) {  // a wave's 64 consecutive children span at most two chunks
+          const u64 k0 = (base_out + base + r0 + (tid & ~63u)) / kChunk;
+          const bool in0 = live && o / kChunk == k0;
+          const u64 s0 = wave_sum64(in0 ? cnt : 0u), s1 = wave_sum64(live && !in0 ? cnt : 0u);
+          if (lane_id() == 0) {
+            if (s0) atomicAdd((unsigned long long*)&nsum[k0], (unsigned long long)s0);
+            if (s1) atomicAdd((unsigned long long*)&nsum[k0 + 1], (unsigned long long)s1);
+          }
+        }
       }
     }
     __syncthreads();  // par/slot reused by the next chunk
@@ -1158,17 +1185,18 @@ hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* n
 }
 
 hipError_t launch_chunk_scan(hipStream_t st, const u64* chunk_sum, const Range* rng, u64* chunk_base, Range* next,
-                             u64 cap, PerftResult* res, int select_path, u64 guard) {
+                             u64 cap, PerftResult* res, int select_path, u64 guard, u64* zero_next, u64 zero_max) {
   hipLaunchKernelGGL(k_chunk_scan, dim3(1), dim3(kTopThreads), 0, st, chunk_sum, rng, chunk_base, next, cap, res,
-                     select_path, guard);
+                     select_path, guard, zero_next, zero_max);
   return hipGetLastError();
 }
 
 hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
                               const uint16_t* tags, const Range* rng, u64 n_bound, const u32* counts,
-                              const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap) {
+                              const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap,
+                              u32* next_counts, u64* next_sum) {
   DC_LAUNCH_RULES_STM(k_level_write, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, counts, chunk_base,
-                      out, out_meta, out_tags, cap, (u32*)nullptr);
+                      out, out_meta, out_tags, cap, (u32*)nullptr, next_counts, next_sum);
   return hipGetLastError();
 }
 
@@ -1330,7 +1358,7 @@ hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const
   auto k = stm ? k_level_write<RefRules, 1, true> : k_level_write<RefRules, 0, true>;
   hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, grid_for(std::min<u64>(n_bound, kMoveWordNodes), kChunk))),
                      dim3(256), 0, st, nodes, nullptr, nullptr, rng, counts, chunk_base, nullptr, nullptr, nullptr,
-                     mw_cap, mw);
+                     mw_cap, mw, nullptr, nullptr);
   return hipGetLastError();
 }
 

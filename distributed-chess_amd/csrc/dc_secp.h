@@ -581,14 +581,6 @@ SECP_HD bool sc_signed128(u32 (&m)[4], const Sc& r) {
   return neg;
 }
 
-// radix-16 Booth digit w (0..32) of a 128-bit magnitude: in [-8, 8], no carries:
-// d_w = b[4w..4w+3] + b[4w-1] - 16 b[4w+3]
-SECP_HD int booth16(const u32 (&m)[4], int w) {
-  const u32 lo = w < 32 ? (m[w >> 3] >> (4 * (w & 7))) & 15u : 0u;
-  const u32 below = w > 0 ? (m[(w - 1) >> 3] >> (4 * ((w - 1) & 7) + 3)) & 1u : 0u;
-  return (int)(lo + below) - (int)((lo & 8u) << 1);
-}
-
 // ------------------------------------------------------------------ points
 SECP_HD void gej_set_ge(Gej& r, const Ge& a) {
   r.x = a.x;
@@ -783,56 +775,115 @@ SECP_HD bool ge_set_xo(Ge& r, const Fe& x, bool odd) {
 constexpr int kGTabRows = 32;
 constexpr int kGTabEntries = kGTabRows * 256;
 
-// u1 G + u2 Q.  Q part: GLV (u2 = k1 + lambda k2, |k_i| < 2^128), radix-16
-// Booth digits over an 8-entry Jacobian table of Q's multiples, lambda applied
-// per lookup as beta X: 128 doublings and 66 additions instead of 256 and 64.
-// G part: the byte table (32 mixed additions, no doublings).
-struct Gj3 {  // Jacobian point known not to be infinity
-  Fe x, y, z;
-};
-SECP_HD void ecmult(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* gtab) {
+// u1 G + u2 Q.  Q part: GLV (u2 = k1 + lambda k2, |k_i| < 2^128), signed
+// radix-2^W Booth digits in [-2^(W-1), 2^(W-1)] over a table of Q's first
+// K = 2^(W-1) multiples, lambda applied per lookup as beta x.  The table is
+// made affine with one batch inversion (Montgomery's trick) so every Q
+// addition is a mixed one (7M + 4S instead of 11M + 5S), and it is read by a
+// select over all K entries (v_cndmask), never by a per-lane index: a
+// per-lane-indexed table lives in scratch (round 1: 8 Jacobian entries,
+// 848 B/lane, 13 GB of HBM traffic per 262k-transaction launch).
+// W = 3: 4 entries (64 VGPRs), 43 windows x 2 halves; W = 4: 8 entries (128 VGPRs),
+// 33 windows.  G part: the byte table (32 mixed additions, no doublings).
+#ifndef DC_SECP_QW
+#define DC_SECP_QW 3
+#endif
+constexpr int kQWindow = DC_SECP_QW;
+
+// bits [pos, pos + len) of the 128-bit magnitude m (zero beyond bit 127)
+SECP_HD u32 bits128(const u32 (&m)[4], int pos, int len) {
+  const int i = pos >> 5, s = pos & 31;
+  u32 v = i < 4 ? m[i] >> s : 0u;
+  if (s + len > 32 && i + 1 < 4) v |= m[i + 1] << (32 - s);
+  return v & ((1u << len) - 1u);
+}
+
+// radix-2^W Booth digit w of m: d_w = b[Ww..Ww+W-1] + b[Ww-1] - 2^W b[Ww+W-1]
+template <int W>
+SECP_HD int booth_digit(const u32 (&m)[4], int w) {
+  const u32 lo = bits128(m, W * w, W);
+  const u32 below = w > 0 ? bits128(m, W * w - 1, 1) : 0u;
+  return (int)(lo + below) - (int)((lo >> (W - 1)) << W);
+}
+
+template <int W>
+SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* gtab) {
+  constexpr int K = 1 << (W - 1);
+  constexpr int NW = (129 + W - 1) / W;  // windows: |k| < 2^128 plus the Booth sign bit
   Sc k1, k2;
   sc_split_lambda(k1, k2, u2);
   u32 m1[4], m2[4];
   const bool n1 = sc_signed128(m1, k1), n2 = sc_signed128(m2, k2);
-  Gj3 tbl[8];  // tbl[i] = (i + 1) Q
+  // (i + 1) Q, i < K, Jacobian (none is infinity: Q has order n), then affine
+  Ge tab[K];
   {
-    Gej t, a;
+    Fe X[K], Y[K], Z[K];
+    Gej a, t;
     gej_set_ge(a, q);
-    tbl[0] = {a.x, a.y, a.z};
-    gej_double(t, a);
-    tbl[1] = {t.x, t.y, t.z};
-    for (int i = 2; i < 8; ++i) {
+    X[0] = a.x;
+    Y[0] = a.y;
+    Z[0] = a.z;
+    if (K > 1) {
+      gej_double(t, a);
+      X[1] = t.x;
+      Y[1] = t.y;
+      Z[1] = t.z;
+    }
+#pragma unroll
+    for (int i = 2; i < K; ++i) {
       gej_add_ge(a, t, q);
-      tbl[i] = {a.x, a.y, a.z};
+      X[i] = a.x;
+      Y[i] = a.y;
+      Z[i] = a.z;
       t = a;
+    }
+    // batch inversion of Z[0..K): prefix products, one inversion, back-substitution
+    Fe c[K];
+    c[0] = Z[0];
+#pragma unroll
+    for (int i = 1; i < K; ++i) fe_mul(c[i], c[i - 1], Z[i]);
+    Fe inv;
+    fe_inv(inv, c[K - 1]);
+#pragma unroll
+    for (int i = K - 1; i >= 0; --i) {
+      Fe zi;
+      if (i > 0) {
+        fe_mul(zi, inv, c[i - 1]);
+        fe_mul(inv, inv, Z[i]);
+      } else {
+        zi = inv;
+      }
+      Fe zi2, zi3;
+      fe_sqr(zi2, zi);
+      fe_mul(zi3, zi2, zi);
+      fe_mul(tab[i].x, X[i], zi2);
+      fe_mul(tab[i].y, Y[i], zi3);
     }
   }
   Fe beta;
   fe_beta(beta);
   Gej acc;
   gej_set_inf(acc);
-  for (int w = 32; w >= 0; --w) {
-    if (w < 32) {
-      gej_double(acc, acc);
-      gej_double(acc, acc);
-      gej_double(acc, acc);
-      gej_double(acc, acc);
+  for (int w = NW - 1; w >= 0; --w) {
+    if (w < NW - 1) {
+#pragma unroll
+      for (int k = 0; k < W; ++k) gej_double(acc, acc);
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int d = booth16(h ? m2 : m1, w);
+      const int d = booth_digit<W>(h ? m2 : m1, w);
       if (d) {
-        const Gj3& e = tbl[(d < 0 ? -d : d) - 1];
-        Gej p;
-        p.x = e.x;
-        p.y = e.y;
-        p.z = e.z;
-        p.inf = 0;
+        const int ad = d < 0 ? -d : d;
+        Ge p = tab[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i) {  // select, not an index: the table stays in VGPRs
+          sel8(p.x.v, ad == i + 1, tab[i].x.v, p.x.v);
+          sel8(p.y.v, ad == i + 1, tab[i].y.v, p.y.v);
+        }
         if (h) fe_mul(p.x, p.x, beta);
         if ((d < 0) != (h ? n2 : n1)) fe_neg(p.y, p.y);
         Gej t;
-        gej_add(t, acc, p);
+        gej_add_ge(t, acc, p);
         acc = t;
       }
     }
@@ -847,6 +898,10 @@ SECP_HD void ecmult(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* g
     }
   }
   r = acc;
+}
+
+SECP_HD void ecmult(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* gtab) {
+  ecmult_w<kQWindow>(r, q, u2, u1, gtab);
 }
 
 // libsecp256k1 verify_raw: r, s in [1, n); z the message scalar.

@@ -24,6 +24,9 @@
 namespace dc {
 
 constexpr u32 kTxThreads = 128;
+#ifndef DC_TX_MINW
+#define DC_TX_MINW 3  // waves per SIMD the register budget allows (168 VGPRs)
+#endif
 
 __global__ __launch_bounds__(256) void k_secp_gtab(secp::Ge* __restrict__ gtab) {
   const int k = (int)(blockIdx.x * blockDim.x + threadIdx.x);
@@ -33,7 +36,7 @@ __global__ __launch_bounds__(256) void k_secp_gtab(secp::Ge* __restrict__ gtab) 
   gtab[k] = e;
 }
 
-__global__ __launch_bounds__(kTxThreads) void k_verify_tx(const char* __restrict__ strings, const u32* __restrict__ off,
+__global__ __launch_bounds__(kTxThreads, DC_TX_MINW) void k_verify_tx(const char* __restrict__ strings, const u32* __restrict__ off,
                                                           const u32* __restrict__ actions,
                                                           const int8_t* __restrict__ turns, u32 n,
                                                           const secp::Ge* __restrict__ gtab,
