@@ -128,6 +128,49 @@ constexpr u32 kTopStage = 512;
 // so the enumeration and the children read their parents from LDS: reading
 // them from the previous ply's global output cost a dependent L2 round trip
 // per child (9 per thread at ply 3).
+// Class groups [g0, g0 + ng) of ref_group_moves, in order (g0, ng wave- or
+// lane-varying: a switch per group).
+template <int STM, class V>
+__device__ __forceinline__ void ref_groups_moves(const Board& b, u32 g0, u32 ng, V&& visit) {
+  for (u32 g = g0; g < g0 + ng; ++g) {
+    switch (g) {
+      case 0: ref_group_moves<STM, 0>(b, visit); break;
+      case 1: ref_group_moves<STM, 1>(b, visit); break;
+      case 2: ref_group_moves<STM, 2>(b, visit); break;
+      default: ref_group_moves<STM, 3>(b, visit); break;
+    }
+  }
+}
+template <int STM>
+__device__ __forceinline__ u32 ref_groups_count(const Board& b, u32 g0, u32 ng) {
+  u32 c = 0;
+  for (u32 g = g0; g < g0 + ng; ++g) {
+    switch (g) {
+      case 0: c += ref_group_count<STM, 0>(b); break;
+      case 1: c += ref_group_count<STM, 1>(b); break;
+      case 2: c += ref_group_count<STM, 2>(b); break;
+      default: c += ref_group_count<STM, 3>(b); break;
+    }
+  }
+  return c;
+}
+
+// REF plies of at most kTopGroupNodes nodes split each node's moves over the
+// four class groups of ref_group_moves: thread t takes groups
+// [g0, g0 + ng) of node t % NB, with NB = 256 nodes per group (ng = 1) when
+// n <= 256, else NB = 512 (ng = 2), so every wave runs one group's code (no
+// divergence between groups).  A node's offset comes from a block scan of the
+// node totals (the group counts summed in LDS) and a group's from the counts
+// of the node's earlier groups: the children keep ref_for_each_move's
+// class-major order.  One lane walking all of a node's moves took 3.5 / 4.2 /
+// 5.6 us to enumerate plies 1 / 2 / 3 of startpos (tools/top_trace.py, round 2;
+// splitting a node's groups over adjacent lanes of one wave was slower still).
+constexpr u32 kTopGroupNodes = 512;
+// Scratch of the grouped count in the (not yet used) slot array: per-thread
+// group counts [0, 1024) and node offsets [1024, 1536).
+__device__ __forceinline__ u32* gcnt_of(u32* slots) { return slots; }
+__device__ __forceinline__ u32* node_off_of(u32* slots) { return slots + kTopThreads; }
+
 template <class R, int STM>
 __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_meta, const uint16_t* cur_tags, u64 n,
                                           Board* nxt, uint16_t* nxt_meta, uint16_t* nxt_tags, u64 cap, bool root,
@@ -136,22 +179,50 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
   const u32 t = threadIdx.x;
   DC_TOP_STAMP(ply, 0);
   const bool stage = n <= kTopStage;
+  const bool grp = !R::kMeta && n <= kTopGroupNodes;  // (kTopGroupNodes <= kTopStage: grouped plies are staged)
+  const u32 NB = n <= 256 ? 256u : 512u, ng = NB / 256u;
+  const u32 gnode = t % NB, g0 = (t / NB) * ng;
   const u64 k = (n + kTopThreads - 1) / kTopThreads;
-  const u64 lo = min(n, (u64)t * k), hi = min(n, lo + k);
+  const u64 lo = grp ? min(n, (u64)gnode) : min(n, (u64)t * k);
+  const u64 hi = grp ? min(n, (u64)gnode + 1) : min(n, lo + k);
   u64 mine = 0;
   for (u64 i = lo; i < hi; ++i) {
     const Board bi = cur[i];
     const u32 mi = load_meta<R>(cur_meta, i);
-    if (stage) {
+    if (stage && (!grp || g0 == 0)) {
       spar[i] = bi;
       if constexpr (R::kMeta) smeta[i] = (uint16_t)mi;
       stags[i] = root ? (uint16_t)0 : cur_tags[i];
     }
-    mine += R::template count<STM>(bi, mi);
+    if constexpr (!R::kMeta) {
+      if (grp) mine += ref_groups_count<STM>(bi, g0, ng);
+      else mine += R::template count<STM>(bi, mi);
+    } else {
+      mine += R::template count<STM>(bi, mi);
+    }
   }
   DC_TOP_STAMP(ply, 1);
-  u64 total;
-  const u64 o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);  // its barriers publish the staging
+  u64 total, o;
+  if (grp) {
+    // group counts -> LDS (gcnt[g * NB + node], in the slot array), node totals
+    // scanned in node order, then each lane's offset within its node
+    gcnt_of(slots)[t] = (u32)mine;
+    __syncthreads();
+    u64 ntot = 0;
+    if (t < n)
+      for (u32 g = 0; g < 4 / ng; ++g) ntot += gcnt_of(slots)[g * NB + t];
+    const u64 nodeoff = block_excl_scan64<kTopThreads / 64>(ntot, wsum, &total);
+    if (t < n) node_off_of(slots)[t] = (u32)nodeoff;
+    __syncthreads();
+    o = 0;
+    if (lo < hi) {
+      o = node_off_of(slots)[gnode];
+      for (u32 g = 0; g < t / NB; ++g) o += gcnt_of(slots)[g * NB + gnode];
+    }
+    __syncthreads();  // gcnt / node_off live in the slot array, which the enumeration overwrites
+  } else {
+    o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);  // its barriers publish the staging
+  }
   DC_TOP_STAMP(ply, 2);
   if (t == 0) *s_total = total;
   if (total > cap) return;  // caller flags overflow
@@ -165,10 +236,17 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
     if (o < wb + kTopSlots && o + mine > wb) {
       u64 j = o;
       for (u64 i = lo; i < hi; ++i) {
-        R::template for_each<STM>(par[i], pmeta(i), [&](int f, int to, int promo) {
+        auto put = [&](int f, int to, int promo) {
           if (j >= wb && j < wb + kTopSlots) slots[j - wb] = ((u32)i << 15) | (u32)f | ((u32)to << 6) | ((u32)promo << 12);
           ++j;
-        });
+        };
+        if constexpr (!R::kMeta) {
+          if (grp) {
+            ref_groups_moves<STM>(par[i], g0, ng, [&](int f, int to) { put(f, to, 0); });
+            continue;
+          }
+        }
+        R::template for_each<STM>(par[i], pmeta(i), put);
       }
     }
     __syncthreads();
@@ -350,15 +428,12 @@ struct WriteShared {
   uint16_t ptag[256];
 };
 
-// MW (REF, k_count3c's input): instead of the child's board and tag, its move
-// word {parent index relative to the level << 12 | f | t << 6} goes to
-// mw[chunk_base + slot] (4 instead of 34 bytes per child, same coalescing).
-template <class R, int STM, bool MW = false>
+template <class R, int STM>
 __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                         const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                         const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
                                                         Board* __restrict__ out, uint16_t* __restrict__ out_meta,
-                                                        uint16_t* __restrict__ out_tags, u64 cap, u32* __restrict__ mw = nullptr,
+                                                        uint16_t* __restrict__ out_tags, u64 cap,
                                                         u32* __restrict__ ncounts = nullptr, u64* __restrict__ nsum = nullptr) {
   __shared__ WriteShared sh;
   const u32 tid = threadIdx.x;
@@ -384,11 +459,9 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
     if (valid) {
       p = load_board(nodes, i);
       pm = load_meta<R>(meta, i);
-      if constexpr (!MW) {
-        sh.par[tid] = p;
-        if constexpr (R::kMeta) sh.pmeta[tid] = pm;
-        sh.ptag[tid] = tags[i];
-      }
+      sh.par[tid] = p;
+      if constexpr (R::kMeta) sh.pmeta[tid] = pm;
+      sh.ptag[tid] = tags[i];
     }
     for (u32 wb = 0; wb < total; wb += kWriteCap) {
       if (wb) __syncthreads();  // previous window fully consumed
@@ -413,24 +486,20 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
         if (live) {
           const u32 e = sh.slot[r];
           const u32 pl = e >> 15;
-          if constexpr (MW) {
-            mw[o] = ((u32)(c * kChunk + pl) << 12) | (e & 0xFFFu);
-          } else {
-            Board ch = sh.par[pl];
-            const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
-                                                 (int)((e >> 12) & 7));
-            store_board(out, o, ch);
-            if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
-            out_tags[o] = sh.ptag[pl];
-            // ncounts (the next level is counted here, not by k_level_count):
-            // the child's own move count, added into its 256-node chunk's sum
-            if (ncounts) {
-              cnt = R::template count<1 - STM>(ch, cm);
-              ncounts[o] = cnt;
-            }
+          Board ch = sh.par[pl];
+          const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
+                                               (int)((e >> 12) & 7));
+          store_board(out, o, ch);
+          if constexpr (R::kMeta) out_meta[o] = (uint16_t)cm;
+          out_tags[o] = sh.ptag[pl];
+          // ncounts (the next level is counted here, not by k_level_count):
+          // the child's own move count, added into its 256-node chunk's sum
+          if (ncounts) {
+            cnt = R::template count<1 - STM>(ch, cm);
+            ncounts[o] = cnt;
           }
         }
-        if (!MW && ncounts) {  // a wave's 64 consecutive children span at most two chunks
+        if (ncounts) {  // a wave's 64 consecutive children span at most two chunks
           const u64 k0 = (base_out + base + r0 + (tid & ~63u)) / kChunk;
           const bool in0 = live && o / kChunk == k0;
           const u64 s0 = wave_sum64(in0 ? cnt : 0u), s1 = wave_sum64(live && !in0 ? cnt : 0u);
@@ -442,6 +511,95 @@ __global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict_
       }
     }
     __syncthreads();  // par/slot reused by the next chunk
+  }
+}
+
+// k_count3c's input (REF): every child of the level `rng` as one u32 move word
+// {parent index relative to the level << 12 | f | t << 6} at its scan offset
+// (4 instead of 34 bytes per child).  A block takes a quarter of a 256-parent
+// chunk (64 parents) and its four waves take the four class groups of
+// ref_group_moves (pawns, knights, king + orthogonal rays, diagonal rays), one
+// lane per parent: a lane walks about a quarter of its position's moves.
+// (Round 2's first version, k_level_write<MW>, had one lane walk all of a
+// parent's ~25 moves: 7.4 us of a median block's 10.9 us, the slowest block
+// 21.5 us -- tools/lw_trace.py.)  Words go through LDS slots so the global
+// stores stay coalesced.
+constexpr u32 kMwParents = 64;
+constexpr u32 kMwCap = kMwParents * 48;  // word slots per window (a quarter averages ~25 per parent)
+
+struct MwShared {
+  u32 slot[kMwCap];
+  u32 gcnt[4][kMwParents];
+  u32 sexcl[kChunk];
+  u64 wsum[4];
+};
+
+template <int STM>
+__global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ nodes, const Range* __restrict__ rng,
+                                                     const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
+                                                     u32* __restrict__ mw, u64 cap) {
+  __shared__ MwShared sh;
+  const u32 tid = threadIdx.x, g = tid >> 6, lane = lane_id();
+  const u64 lo = rng->lo, hi = rng->hi;
+  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
+  for (u64 item = blockIdx.x; item < nch * 4; item += gridDim.x) {
+    const u64 c = item >> 2;
+    const u32 q = (u32)(item & 3);
+    // every global load of the item issues before the scan's barriers
+    const u64 ic = lo + c * kChunk + tid;
+    const u32 cnt = ic < hi ? counts[ic - lo] : 0u;
+    const u32 pl = q * kMwParents + lane;  // this lane's parent within the chunk
+    const u64 i = lo + c * kChunk + pl;
+    const bool valid = i < hi;
+    Board p{0, 0, 0, 0};
+    if (valid) p = load_board(nodes, i);
+    const u64 cbase = chunk_base[c];
+    // the chunk's exclusive move offsets (each quarter's block scans the chunk)
+    u64 tot64;
+    sh.sexcl[tid] = (u32)block_excl_scan64<4>(cnt, sh.wsum, &tot64);
+    u32 gc = 0;  // moves of this wave's class group
+    if (valid) {
+      switch (g) {  // wave-uniform
+        case 0: gc = ref_group_count<STM, 0>(p); break;
+        case 1: gc = ref_group_count<STM, 1>(p); break;
+        case 2: gc = ref_group_count<STM, 2>(p); break;
+        default: gc = ref_group_count<STM, 3>(p); break;
+      }
+    }
+    sh.gcnt[g][lane] = gc;
+    __syncthreads();
+    const u32 qbase = sh.sexcl[q * kMwParents];
+    const u32 qend = q == 3 ? (u32)tot64 : sh.sexcl[(q + 1) * kMwParents];
+    u32 goff = sh.sexcl[pl] - qbase;
+    for (u32 k = 0; k < g; ++k) goff += sh.gcnt[k][lane];
+    const u32 qtotal = qend - qbase;
+    const u64 base_out = cbase + qbase;
+    for (u32 wb = 0; wb < qtotal; wb += kMwCap) {
+      if (wb) __syncthreads();  // the previous window is written out
+      u32 j = goff;
+      if (valid && gc && j < wb + kMwCap && j + gc > wb) {
+        auto put = [&](int f, int t) {
+          if (j >= wb && j - wb < kMwCap) sh.slot[j - wb] = (u32)f | ((u32)t << 6) | (pl << 12);
+          ++j;
+        };
+        switch (g) {
+          case 0: ref_group_moves<STM, 0>(p, put); break;
+          case 1: ref_group_moves<STM, 1>(p, put); break;
+          case 2: ref_group_moves<STM, 2>(p, put); break;
+          default: ref_group_moves<STM, 3>(p, put); break;
+        }
+      }
+      __syncthreads();
+      const u32 ns = min(kMwCap, qtotal - wb);
+      for (u32 r = tid; r < ns; r += 256) {
+        const u64 o = base_out + wb + r;
+        if (o < cap) {  // words beyond cap are dropped (the level is flagged)
+          const u32 e = sh.slot[r];
+          mw[o] = ((u32)(c * kChunk + (e >> 12)) << 12) | (e & 0xFFFu);
+        }
+      }
+    }
+    __syncthreads();  // sexcl, gcnt and slot are reused by the next item
   }
 }
 
@@ -1196,7 +1354,7 @@ hipError_t launch_level_write(hipStream_t st, u32 rules, int stm, const Board* n
                               const u64* chunk_base, Board* out, uint16_t* out_meta, uint16_t* out_tags, u64 cap,
                               u32* next_counts, u64* next_sum) {
   DC_LAUNCH_RULES_STM(k_level_write, grid_for(n_bound, kChunk), 256, st, nodes, meta, tags, rng, counts, chunk_base,
-                      out, out_meta, out_tags, cap, (u32*)nullptr, next_counts, next_sum);
+                      out, out_meta, out_tags, cap, next_counts, next_sum);
   return hipGetLastError();
 }
 
@@ -1355,10 +1513,9 @@ hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* 
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
                               const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap) {
   // words beyond mw_cap are dropped (a flagged level is never read)
-  auto k = stm ? k_level_write<RefRules, 1, true> : k_level_write<RefRules, 0, true>;
-  hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, grid_for(std::min<u64>(n_bound, kMoveWordNodes), kChunk))),
-                     dim3(256), 0, st, nodes, nullptr, nullptr, rng, counts, chunk_base, nullptr, nullptr, nullptr,
-                     mw_cap, mw, nullptr, nullptr);
+  auto k = stm ? k_level_moves<1> : k_level_moves<0>;
+  hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, grid_for(std::min<u64>(n_bound, kMoveWordNodes) * 4, kChunk))),
+                     dim3(256), 0, st, nodes, rng, counts, chunk_base, mw, mw_cap);
   return hipGetLastError();
 }
 

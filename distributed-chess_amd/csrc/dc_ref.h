@@ -638,4 +638,92 @@ __device__ __forceinline__ void ref_for_each_move(const Board& b, Visit&& visit)
   slide(ray_attacks<-7, kNotA>(s.D, e) & no, std::integral_constant<int, 7>{});
 }
 
+
+// ref_for_each_move's classes in four contiguous groups (so the groups in
+// order 0..3 give ref_for_each_move's order): 0 pawns (push1, push2, both
+// captures), 1 knights, 2 king + orthogonal rays, 3 diagonal rays.
+// ref_group_count<STM, G> = the number of moves ref_group_moves<STM, G> visits.
+// k_level_moves enumerates one group per wave, so a lane walks a quarter of
+// its position's moves.
+template <int STM, int G, class Visit>
+__device__ __forceinline__ void ref_group_moves(const Board& b, Visit&& visit) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 no = s.notown, e = s.empty;
+  auto leap = [&](u64 targets, int delta) {
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(t - delta, t);
+    }
+  };
+  auto slide = [&](u64 targets, auto dtag) {
+    constexpr int D = decltype(dtag)::value;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(slider_source<D>(s.occ, t), t);
+    }
+  };
+  if constexpr (G == 0) {
+    const u64 push1 = sh<PD::F>(s.P) & e;
+    leap(push1, PD::F);
+    leap(sh<PD::F>(push1 & PD::ROW_AFTER1) & e, 2 * PD::F);
+    leap(sh<PD::CW>(s.P & kNotA) & s.enemy, PD::CW);
+    leap(sh<PD::CE>(s.P & kNotH) & s.enemy, PD::CE);
+  } else if constexpr (G == 1) {
+    const u64 n = s.N;
+    leap(sh<17>(n & kNotH) & no, 17);
+    leap(sh<15>(n & kNotA) & no, 15);
+    leap(sh<10>(n & kNotGH) & no, 10);
+    leap(sh<6>(n & kNotAB) & no, 6);
+    leap(sh<-6>(n & kNotGH) & no, -6);
+    leap(sh<-10>(n & kNotAB) & no, -10);
+    leap(sh<-15>(n & kNotH) & no, -15);
+    leap(sh<-17>(n & kNotA) & no, -17);
+  } else if constexpr (G == 2) {
+    const u64 k = s.K;
+    leap(sh<8>(k) & no, 8);
+    leap(sh<-8>(k) & no, -8);
+    leap(sh<1>(k & kNotH) & no, 1);
+    leap(sh<-1>(k & kNotA) & no, -1);
+    leap(sh<9>(k & kNotH) & no, 9);
+    leap(sh<7>(k & kNotA) & no, 7);
+    leap(sh<-7>(k & kNotH) & no, -7);
+    leap(sh<-9>(k & kNotA) & no, -9);
+    slide(ray_attacks<8, kAll>(s.O, e) & no, std::integral_constant<int, 0>{});
+    slide(ray_attacks<-8, kAll>(s.O, e) & no, std::integral_constant<int, 1>{});
+    slide(ray_attacks<1, kNotA>(s.O, e) & no, std::integral_constant<int, 2>{});
+    slide(ray_attacks<-1, kNotH>(s.O, e) & no, std::integral_constant<int, 3>{});
+  } else {
+    slide(ray_attacks<9, kNotA>(s.D, e) & no, std::integral_constant<int, 4>{});
+    slide(ray_attacks<-9, kNotH>(s.D, e) & no, std::integral_constant<int, 5>{});
+    slide(ray_attacks<7, kNotH>(s.D, e) & no, std::integral_constant<int, 6>{});
+    slide(ray_attacks<-7, kNotA>(s.D, e) & no, std::integral_constant<int, 7>{});
+  }
+}
+
+template <int STM, int G>
+__device__ __forceinline__ u32 ref_group_count(const Board& b) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 no = s.notown, e = s.empty;
+  if constexpr (G == 0) {
+    const u64 push1 = sh<PD::F>(s.P) & e;
+    return pc(push1) + pc(and3(sh<PD::F>(push1), PD::ROW_DBL, e)) + pc(and3(sh<PD::CW>(s.P), kNotH, s.enemy)) +
+           pc(and3(sh<PD::CE>(s.P), kNotA, s.enemy));
+  } else if constexpr (G == 1) {
+    const u64 n = s.N;
+    return pc(and3(sh<17>(n), kNotA, no)) + pc(and3(sh<15>(n), kNotH, no)) + pc(and3(sh<10>(n), kNotAB, no)) +
+           pc(and3(sh<6>(n), kNotGH, no)) + pc(and3(sh<-6>(n), kNotAB, no)) + pc(and3(sh<-10>(n), kNotGH, no)) +
+           pc(and3(sh<-15>(n), kNotA, no)) + pc(and3(sh<-17>(n), kNotH, no));
+  } else if constexpr (G == 2) {
+    return king_moves(s.K, no) + pc(ray_attacks<8, kAll>(s.O, e) & no) + pc(ray_attacks<-8, kAll>(s.O, e) & no) +
+           pc(ray_moves<1, kNotA>(s.O, e, no)) + pc(ray_moves<-1, kNotH>(s.O, e, no));
+  } else {
+    return pc(ray_moves<9, kNotA>(s.D, e, no)) + pc(ray_moves<-9, kNotH>(s.D, e, no)) +
+           pc(ray_moves<7, kNotH>(s.D, e, no)) + pc(ray_moves<-7, kNotA>(s.D, e, no));
+  }
+}
+
 }  // namespace dc
