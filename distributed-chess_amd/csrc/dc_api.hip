@@ -141,6 +141,7 @@ struct dc_ctx {
   DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
   DBuf<u32> move_words;  // k_count3c: the final stage's parents as move words below their grandparents
+  DBuf<u32> top_words;   // k_expand_top's last ply as move words (k_make_count makes it)
   // transaction-signature check: staged strings / offsets / actions / turns,
   // and the G table (built on first use)
   DBuf<char> tx_text;
@@ -167,6 +168,8 @@ struct dc_ctx {
     res.release();
     rng.release();
     desc.release();
+    top_words.release();
+    move_words.release();
     dfs_stack.release();
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (rgraph) (void)hipGraphExecDestroy(rgraph);
@@ -996,10 +999,15 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     *guard = 0;
     return std::min(n_lvl * kBranchBound, kSpecBudget / kNodeBytes);
   };
+  // The target ply of k_expand_top is made on many CUs by k_make_count (it
+  // replaces that level's k_level_count) when that level is counted next.
+  bool top_words = !exact && T >= 2 && T < F && !(sharded && S == T);
+  if (top_words) HIP_TRY(c->top_words.ensure(cap_T));
   // the result block is cleared by k_expand_top itself (its first stores)
   HIP_TRY(c->timed("expand_top", 0, [&] {
     return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, ts, c->nodes[0].p,
-                                 fide ? c->meta[0].p : nullptr, c->tags[0].p, cap_T, c->res.p, c->rng.p + T);
+                                 fide ? c->meta[0].p : nullptr, c->tags[0].p, cap_T, c->res.p, c->rng.p + T,
+                                 top_words ? c->top_words.p : nullptr);
   }));
   u32 L = T;
   u64 nb = cap_T;
@@ -1041,11 +1049,19 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       HIP_TRY(cnt_buf[cb ^ 1]->ensure(std::max<u64>(std::min<u64>(cap, 0xFFFFFFFFull), 1)));
       HIP_TRY(sum_buf[cb ^ 1]->ensure(nch_next));
     }
-    if (!counted)
+    if (top_words) {  // level T, left as move words by k_expand_top
+      top_words = false;
+      HIP_TRY(c->timed("expand_count", 0, [&] {
+        return dc::launch_make_count(c->stream, rules, stm ^ 1, ts.nodes[T - 2], ts.meta[T - 2], ts.tags[T - 2],
+                                     c->top_words.p, c->rng.p + L, nb, c->nodes[buf].p,
+                                     fide ? c->meta[buf].p : nullptr, c->tags[buf].p, cnt_buf[cb]->p, sum_buf[cb]->p);
+      }));
+    } else if (!counted) {
       HIP_TRY(c->timed("expand_count", 0, [&] {
         return dc::launch_level_count(c->stream, rules, stm, c->nodes[buf].p, fide ? c->meta[buf].p : nullptr,
                                       c->rng.p + L, nb, cnt_buf[cb]->p, sum_buf[cb]->p);
       }));
+    }
     HIP_TRY(c->timed("scan", 0, [&] {
       return dc::launch_chunk_scan(c->stream, sum_buf[cb]->p, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, cap,
                                    c->res.p, select_path, guard, count_next ? sum_buf[cb ^ 1]->p : nullptr, nch_next);

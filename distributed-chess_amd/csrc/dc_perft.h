@@ -32,7 +32,14 @@ struct TopScratch {
 
 hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const uint16_t* root_meta, u32 stm0,
                              u32 target, const TopScratch& s, Board* out, uint16_t* out_meta, uint16_t* out_tags,
-                             u64 cap_out, PerftResult* res, Range* out_rng);
+                             u64 cap_out, PerftResult* res, Range* out_rng, u32* words = nullptr);
+// words != nullptr (target ply >= 2): k_expand_top leaves the target ply as
+// move words {parent << 15 | f | t << 6 | promo << 12} over the previous top
+// ply (s.nodes[target - 2]); launch_make_count then makes, stores and counts
+// it (in place of launch_level_count).  stm_par = side to move at the parents.
+hipError_t launch_make_count(hipStream_t st, u32 rules, int stm_par, const Board* par, const uint16_t* par_meta,
+                             const uint16_t* par_tags, const u32* words, const Range* rng, u64 n_bound, Board* out,
+                             uint16_t* out_meta, uint16_t* out_tags, u32* counts, u64* chunk_sum);
 // Per level: count (+ chunk sums), one-workgroup chunk scan (-> next Range), write.
 u64 chunks_for(u64 n);
 hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,

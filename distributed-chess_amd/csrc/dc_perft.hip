@@ -175,7 +175,7 @@ template <class R, int STM>
 __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_meta, const uint16_t* cur_tags, u64 n,
                                           Board* nxt, uint16_t* nxt_meta, uint16_t* nxt_tags, u64 cap, bool root,
                                           PerftResult* res, u64* wsum, u64* s_total, u32* slots, Board* spar,
-                                          uint16_t* smeta, uint16_t* stags, u32 ply) {
+                                          uint16_t* smeta, uint16_t* stags, u32 ply, u32* words = nullptr) {
   const u32 t = threadIdx.x;
   DC_TOP_STAMP(ply, 0);
   const bool stage = n <= kTopStage;
@@ -252,6 +252,10 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
     __syncthreads();
     DC_TOP_STAMP(ply, 3);
     const u32 ns = (u32)min((u64)kTopSlots, total - wb);
+    if (words) {  // the children are made and counted by k_make_count, on many CUs
+      for (u32 r = t; r < ns; r += kTopThreads) words[wb + r] = slots[r];
+      continue;
+    }
     for (u32 r = t; r < ns; r += kTopThreads) {
       const u32 e = slots[r];
       const u32 pl = e >> 15;
@@ -286,7 +290,8 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
                                                              u32 target, TopBufs sb, Board* __restrict__ out,
                                                              uint16_t* __restrict__ out_meta,
                                                              uint16_t* __restrict__ out_tags, u64 cap_out,
-                                                             PerftResult* __restrict__ res, Range* __restrict__ out_rng) {
+                                                             PerftResult* __restrict__ res, Range* __restrict__ out_rng,
+                                                             u32* __restrict__ words) {
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
   __shared__ u32 slots[kTopSlots];
@@ -316,12 +321,13 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
     uint16_t* dm = last ? out_meta : sb.meta[ply - 1];
     uint16_t* dt = last ? out_tags : sb.tags[ply - 1];
     const u64 cap = last ? cap_out : sb.cap[ply - 1];
+    u32* wd = last && ply >= 2 ? words : nullptr;  // target ply as move words (k_make_count makes it)
     if ((stm0 ^ (ply - 1)) & 1)
       top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots, spar, smeta,
-                      stags, ply);
+                      stags, ply, wd);
     else
       top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots, spar, smeta,
-                      stags, ply);
+                      stags, ply, wd);
     __syncthreads();
     DC_TOP_STAMP(ply, 4);
     n = s_total;
@@ -363,6 +369,42 @@ __global__ __launch_bounds__(256) void k_level_count(const Board* __restrict__ n
     u32 cnt = 0;
     if (i < hi) {
       cnt = R::template count<STM>(load_board(nodes, i), load_meta<R>(meta, i));
+      counts[i - lo] = cnt;
+    }
+    u64 tot;
+    block_excl_scan64<4>(cnt, wsum, &tot);
+    if (threadIdx.x == 0) chunk_sum[c] = tot;
+  }
+}
+
+// k_level_count for a level k_expand_top left as move words (words != nullptr
+// there): each child is made from its parent (the previous top ply, still in
+// the top scratch) and stored with its tag before it is counted.  Making the
+// 8,902 ply-3 children of startpos inside the one-workgroup k_expand_top took
+// 7.1 us (tools/top_trace.py); here they spread over 35 blocks.
+// STM = side to move at the parents.
+template <class R, int STM>
+__global__ __launch_bounds__(256) void k_make_count(const Board* __restrict__ par, const uint16_t* __restrict__ par_meta,
+                                                    const uint16_t* __restrict__ par_tags, const u32* __restrict__ words,
+                                                    const Range* __restrict__ rng, Board* __restrict__ out,
+                                                    uint16_t* __restrict__ out_meta, uint16_t* __restrict__ out_tags,
+                                                    u32* __restrict__ counts, u64* __restrict__ chunk_sum) {
+  __shared__ u64 wsum[4];
+  const u64 lo = rng->lo, hi = rng->hi;
+  const u64 nch = (hi - lo + kChunk - 1) / kChunk;
+  for (u64 c = blockIdx.x; c < nch; c += gridDim.x) {
+    const u64 i = lo + c * kChunk + threadIdx.x;
+    u32 cnt = 0;
+    if (i < hi) {
+      const u32 e = words[i];
+      const u32 pl = e >> 15;
+      Board ch = par[pl];
+      const u32 cm = R::template make<STM>(ch, load_meta<R>(par_meta, pl), (int)(e & 63), (int)((e >> 6) & 63),
+                                           (int)((e >> 12) & 7));
+      store_board(out, i, ch);
+      if constexpr (R::kMeta) out_meta[i] = (uint16_t)cm;
+      out_tags[i] = par_tags[pl];
+      cnt = R::template count<1 - STM>(ch, cm);
       counts[i - lo] = cnt;
     }
     u64 tot;
@@ -1139,6 +1181,9 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
   const u64 lo = rng->lo;
   const u32 total = (u32)(rng_ch->hi - rng_ch->lo);  // children (< 2^32: launcher)
   for (;;) {
+    // (fetching the next group's index one group ahead, to take its round
+    // trip off the load chain, made the kernel 0.495 -> 0.519 ms at perft(7):
+    // a block then holds a group it cannot start, which lengthens the tail)
     if (tid == 0) sh.next = atomicAdd(next_group, 1u);
     __syncthreads();
     const u64 s = (u64)sh.next * kGroup;
@@ -1317,7 +1362,7 @@ static u32 resident_grid(K kernel, u32 block, u32 want) {
 
 hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const uint16_t* root_meta, u32 stm0,
                              u32 target, const TopScratch& s, Board* out, uint16_t* out_meta, uint16_t* out_tags,
-                             u64 cap_out, PerftResult* res, Range* out_rng) {
+                             u64 cap_out, PerftResult* res, Range* out_rng, u32* words) {
   TopBufs b;
   for (int k = 0; k < 2; ++k) {
     b.nodes[k] = s.nodes[k];
@@ -1327,10 +1372,10 @@ hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const
   }
   if (rules == 0)
     hipLaunchKernelGGL(k_expand_top<RefRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, b, out,
-                       out_meta, out_tags, cap_out, res, out_rng);
+                       out_meta, out_tags, cap_out, res, out_rng, words);
   else
     hipLaunchKernelGGL(k_expand_top<FideRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, b,
-                       out, out_meta, out_tags, cap_out, res, out_rng);
+                       out, out_meta, out_tags, cap_out, res, out_rng, words);
   return hipGetLastError();
 }
 
@@ -1339,6 +1384,15 @@ u64 chunks_for(u64 n) { return (n + kChunk - 1) / kChunk; }
 hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,
                               const Range* rng, u64 n_bound, u32* counts, u64* chunk_sum) {
   DC_LAUNCH_RULES_STM(k_level_count, grid_for(n_bound, kChunk), 256, st, nodes, meta, rng, counts, chunk_sum);
+  return hipGetLastError();
+}
+
+hipError_t launch_make_count(hipStream_t st, u32 rules, int stm_par, const Board* par, const uint16_t* par_meta,
+                             const uint16_t* par_tags, const u32* words, const Range* rng, u64 n_bound, Board* out,
+                             uint16_t* out_meta, uint16_t* out_tags, u32* counts, u64* chunk_sum) {
+  const int stm = stm_par;
+  DC_LAUNCH_RULES_STM(k_make_count, grid_for(n_bound, kChunk), 256, st, par, par_meta, par_tags, words, rng, out,
+                      out_meta, out_tags, counts, chunk_sum);
   return hipGetLastError();
 }
 
