@@ -166,16 +166,14 @@ __device__ __forceinline__ u32 ref_groups_count(const Board& b, u32 g0, u32 ng) 
 // 5.6 us to enumerate plies 1 / 2 / 3 of startpos (tools/top_trace.py, round 2;
 // splitting a node's groups over adjacent lanes of one wave was slower still).
 constexpr u32 kTopGroupNodes = 512;
-// Scratch of the grouped count in the (not yet used) slot array: per-thread
-// group counts [0, 1024) and node offsets [1024, 1536).
-__device__ __forceinline__ u32* gcnt_of(u32* slots) { return slots; }
-__device__ __forceinline__ u32* node_off_of(u32* slots) { return slots + kTopThreads; }
+
 
 template <class R, int STM>
 __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_meta, const uint16_t* cur_tags, u64 n,
                                           Board* nxt, uint16_t* nxt_meta, uint16_t* nxt_tags, u64 cap, bool root,
                                           PerftResult* res, u64* wsum, u64* s_total, u32* slots, Board* spar,
-                                          uint16_t* smeta, uint16_t* stags, u32 ply, u32* words = nullptr) {
+                                          uint16_t* smeta, uint16_t* stags, u32 ply, u32* gcnt, u32* node_off,
+                                          u32* words = nullptr) {
   const u32 t = threadIdx.x;
   DC_TOP_STAMP(ply, 0);
   const bool stage = n <= kTopStage;
@@ -204,22 +202,35 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
   DC_TOP_STAMP(ply, 1);
   u64 total, o;
   if (grp) {
-    // group counts -> LDS (gcnt[g * NB + node], in the slot array), node totals
-    // scanned in node order, then each lane's offset within its node
-    gcnt_of(slots)[t] = (u32)mine;
+    // group counts -> LDS (gcnt[g * NB + node]), node totals scanned in node
+    // order (by wave 0 alone up to 64 nodes), then each lane's offset within
+    // its node
+    gcnt[t] = (u32)mine;
     __syncthreads();
-    u64 ntot = 0;
-    if (t < n)
-      for (u32 g = 0; g < 4 / ng; ++g) ntot += gcnt_of(slots)[g * NB + t];
-    const u64 nodeoff = block_excl_scan64<kTopThreads / 64>(ntot, wsum, &total);
-    if (t < n) node_off_of(slots)[t] = (u32)nodeoff;
-    __syncthreads();
+    if (n <= 64) {
+      if (t < 64) {
+        u64 ntot = 0;
+        if (t < n)
+          for (u32 g = 0; g < 4 / ng; ++g) ntot += gcnt[g * NB + t];
+        const u64 incl = wave_incl_scan64(ntot);
+        node_off[t] = (u32)(incl - ntot);
+        if (t == 63) wsum[0] = incl;
+      }
+      __syncthreads();
+      total = wsum[0];
+    } else {
+      u64 ntot = 0;
+      if (t < n)
+        for (u32 g = 0; g < 4 / ng; ++g) ntot += gcnt[g * NB + t];
+      const u64 nodeoff = block_excl_scan64<kTopThreads / 64>(ntot, wsum, &total);
+      if (t < n) node_off[t] = (u32)nodeoff;
+      __syncthreads();
+    }
     o = 0;
     if (lo < hi) {
-      o = node_off_of(slots)[gnode];
-      for (u32 g = 0; g < t / NB; ++g) o += gcnt_of(slots)[g * NB + gnode];
+      o = node_off[gnode];
+      for (u32 g = 0; g < t / NB; ++g) o += gcnt[g * NB + gnode];
     }
-    __syncthreads();  // gcnt / node_off live in the slot array, which the enumeration overwrites
   } else {
     o = block_excl_scan64<kTopThreads / 64>(mine, wsum, &total);  // its barriers publish the staging
   }
@@ -295,6 +306,8 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
   __shared__ u32 slots[kTopSlots];
+  __shared__ u32 gcnt[kTopThreads];         // grouped plies: per-thread group counts
+  __shared__ u32 node_off[kTopGroupNodes];  // ... and node offsets
   __shared__ Board spar[kTopStage];
   __shared__ uint16_t smeta[R::kMeta ? kTopStage : 1];
   __shared__ uint16_t stags[kTopStage];
@@ -324,10 +337,10 @@ __global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restr
     u32* wd = last && ply >= 2 ? words : nullptr;  // target ply as move words (k_make_count makes it)
     if ((stm0 ^ (ply - 1)) & 1)
       top_level<R, 1>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots, spar, smeta,
-                      stags, ply, wd);
+                      stags, ply, gcnt, node_off, wd);
     else
       top_level<R, 0>(cur, cur_meta, cur_tags, n, dst, dm, dt, cap, ply == 1, res, wsum, &s_total, slots, spar, smeta,
-                      stags, ply, wd);
+                      stags, ply, gcnt, node_off, wd);
     __syncthreads();
     DC_TOP_STAMP(ply, 4);
     n = s_total;
