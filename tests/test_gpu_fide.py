@@ -104,3 +104,11 @@ def test_gen_and_replay_fide(engine):
 def test_perft7_startpos_fide(engine):
     """SURVEY §8d C5 (FIDE half) on one GPU: published 3,195,901,860."""
     assert engine.perft(dchess.startpos(), 7, rules=FIDE)[0] == OG["perft_fide"]["startpos"]["perft"]["7"]
+
+
+@pytest.mark.parametrize("depth,n_shards,split", [(6, 3, 4), (6, 2, 3)])
+def test_perft_startpos_fide_shards(engine, depth, n_shards, split):
+    """FIDE through the same front end (k_make_count with FideRules, strided
+    shards cut at ply 3 or 4): the shards sum to the published perft."""
+    t = sum(engine.perft_shard(dchess.startpos(), depth, split, k, n_shards, rules=FIDE)[0] for k in range(n_shards))
+    assert t == OG["perft_fide"]["startpos"]["perft"][str(depth)]

@@ -17,6 +17,7 @@ pytestmark = pytest.mark.gpu
 GOLD = os.path.join(os.path.dirname(__file__), "golden")
 KA = json.load(open(os.path.join(GOLD, "known_answers.json")))
 OG = json.load(open(os.path.join(GOLD, "oracle_golden.json")))
+REF_DEEP = json.load(open(os.path.join(GOLD, "ref_deep.json")))
 
 
 def sha(a):
@@ -340,6 +341,24 @@ def test_perft_shards_sum(engine, n_shards, split):
         acc += sd
         t += st
     assert t == tot and (acc == div).all()
+
+
+@pytest.mark.parametrize("depth,n_shards,split", [(6, 3, 4), (7, 4, 4), (7, 3, 5), (6, 2, 3), (8, 2, 4)])
+def test_perft_deep_shards_golden(engine, depth, n_shards, split):
+    """Strided shards cut after the top kernel (split 3), after k_make_count's
+    level (4) or at the final stage's parents (5: k_count2c instead of
+    k_count3c), at depths where k_expand_top leaves ply 3 as move words and a
+    level write counts the next level: the shards' divides sum to the golden."""
+    s = dchess.startpos()
+    g = OG["perft_ref"]["startpos"][str(depth)] if depth <= 7 else REF_DEEP["startpos_d8"]
+    acc, t = {}, 0
+    for k in range(n_shards):
+        st, sd, srm = engine.perft_shard(s, depth, split, k, n_shards)
+        t += st
+        for m, v in zip(srm, sd):
+            acc[str(int(m))] = acc.get(str(int(m)), 0) + int(v)
+    assert t == g["total"]
+    assert acc == {str(k): int(v) for k, v in g["divide"].items()}
 
 
 @pytest.mark.parametrize("depth,n_shards", [(5, 1), (6, 1), (6, 3), (3, 2)])
