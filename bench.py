@@ -490,8 +490,10 @@ def validate_latency(eng, calls=2000):
     us = ts * 1e6
     return {"calls": calls, "median_us": float(np.median(us)), "p99_us": float(np.percentile(us, 99)),
             "min_us": float(us.min()), "unit": "microseconds per dc_validate_batch(n=1) call",
-            "note": "host-memory call incl. H2D, kernel, D2H and stream sync; the reference's liveness budget is "
-                    "the 10 s view timeout (core/src/main.rs:30)"}
+            "note": "host-memory call: the batch staged in a pinned block the kernel reads and writes in place "
+                    "(no DMA copies), one launch, completion seen through a flag the kernel publishes to that "
+                    "block (no stream sync); the reference's liveness budget is the 10 s view timeout "
+                    "(core/src/main.rs:30)"}
 
 
 def state_hash_leg(eng, d, args):

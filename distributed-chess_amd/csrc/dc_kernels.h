@@ -51,9 +51,9 @@ __host__ __device__ inline void startpos_board(B& b) {
   b.b3 = kStartB3;
 }
 
-hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out);
+hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out, u32* done = nullptr, u32 seq = 0);
 hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
-                            uint8_t* info);
+                            uint8_t* info, u32* done = nullptr, u32 seq = 0);
 // stats[5] = validated, accepted, rejected, digest sum, digest xor; partial has
 // replay_partials(n_games) x 5 u64 of scratch.  *host_written: the five
 // counters were also stored into pinned `stats_host` (valid once the stream is

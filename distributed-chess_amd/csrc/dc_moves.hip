@@ -13,19 +13,32 @@
 namespace dc {
 
 // ------------------------------------------------------------- validation
-__global__ __launch_bounds__(256) void k_validate_ref(const DevPos* __restrict__ pos, const uint16_t* __restrict__ moves,
-                                                      u32 n, uint8_t* __restrict__ out) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const DevPos p = pos[i];
-  const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
-  out[i] = (uint8_t)ref_verdict(b, p.stm & 1, moves[i]);
+// done != nullptr (a one-block launch whose I/O is pinned host memory, dc_api
+// HostIo): once the block's results are stored, thread 0 publishes seq to the
+// host flag with a system-scope release, so the caller can spin on the flag
+// instead of synchronising the stream (the live n = 1 consensus call).
+__device__ __forceinline__ void publish_done(u32* done, u32 seq) {
+  if (!done) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {  // a divergent (vector) store
+    __threadfence_system();
+    __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
-__global__ __launch_bounds__(256) void k_apply_ref(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 n,
-                                                   uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info) {
+__global__ __launch_bounds__(256) void k_validate_ref(const DevPos* __restrict__ pos, const uint16_t* __restrict__ moves,
+                                                      u32 n, uint8_t* __restrict__ out, u32* done, u32 seq) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  if (i < n) {
+    const DevPos p = pos[i];
+    const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+    out[i] = (uint8_t)ref_verdict(b, p.stm & 1, moves[i]);
+  }
+  publish_done(done, seq);
+}
+
+__device__ __forceinline__ void apply_ref_one(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 i,
+                                              uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info) {
   DevPos p = pos[i];
   Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
   const u32 m = moves[i];
@@ -50,6 +63,14 @@ __global__ __launch_bounds__(256) void k_apply_ref(DevPos* __restrict__ pos, con
   p.bb[3] = b.b3;
   p.stm ^= 1;
   pos[i] = p;
+}
+
+__global__ __launch_bounds__(256) void k_apply_ref(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 n,
+                                                   uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info, u32* done,
+                                                   u32 seq) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) apply_ref_one(pos, moves, i, verdicts, info);
+  publish_done(done, seq);
 }
 
 // Replay counters: one partial record {validated, accepted, rejected, digest
@@ -682,18 +703,18 @@ __global__ __launch_bounds__(256) void k_gen_games_ref_v1(u64 seed, u64 first_ga
 
 // ------------------------------------------------------------- FIDE (K1/K2/K5)
 __global__ __launch_bounds__(256) void k_validate_fide(const DevPos* __restrict__ pos, const uint16_t* __restrict__ moves,
-                                                       u32 n, uint8_t* __restrict__ out) {
+                                                       u32 n, uint8_t* __restrict__ out, u32* done, u32 seq) {
   const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const DevPos p = pos[i];
-  const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
-  out[i] = (uint8_t)fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), moves[i]);
+  if (i < n) {
+    const DevPos p = pos[i];
+    const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+    out[i] = (uint8_t)fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), moves[i]);
+  }
+  publish_done(done, seq);
 }
 
-__global__ __launch_bounds__(256) void k_apply_fide(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 n,
-                                                    uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info) {
-  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+__device__ __forceinline__ void apply_fide_one(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 i,
+                                               uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info) {
   DevPos p = pos[i];
   Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
   const u32 m = moves[i];
@@ -720,6 +741,14 @@ __global__ __launch_bounds__(256) void k_apply_fide(DevPos* __restrict__ pos, co
   p.castle = (uint8_t)(nm & 15);
   p.ep = (nm & META_EP_VALID) ? (int8_t)((nm >> 4) & 63) : (int8_t)-1;
   pos[i] = p;
+}
+
+__global__ __launch_bounds__(256) void k_apply_fide(DevPos* __restrict__ pos, const uint16_t* __restrict__ moves, u32 n,
+                                                    uint8_t* __restrict__ verdicts, uint8_t* __restrict__ info, u32* done,
+                                                    u32 seq) {
+  const u32 i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) apply_fide_one(pos, moves, i, verdicts, info);
+  publish_done(done, seq);
 }
 
 __global__ __launch_bounds__(256) void k_replay_fide(Board start, u32 stm0, u32 meta0, const uint16_t* __restrict__ moves,
@@ -789,16 +818,19 @@ __global__ __launch_bounds__(256) void k_gen_games_fide(u64 seed, u64 first_game
 
 // ------------------------------------------------------------- launchers
 
-hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out) {
+hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out, u32* done,
+                               u32 seq) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_validate_ref, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, out);
+  if (done && n > 256) return hipErrorInvalidValue;  // the flag is published by a single block
+  hipLaunchKernelGGL(k_validate_ref, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, out, done, seq);
   return hipGetLastError();
 }
 
 hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
-                            uint8_t* info) {
+                            uint8_t* info, u32* done, u32 seq) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_apply_ref, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, verdicts, info);
+  if (done && n > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_apply_ref, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, verdicts, info, done, seq);
   return hipGetLastError();
 }
 
@@ -894,15 +926,18 @@ hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_
   return hipGetLastError();
 }
 
-hipError_t launch_validate_fide(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out) {
+hipError_t launch_validate_fide(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out, u32* done,
+                                u32 seq) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_validate_fide, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, out);
+  if (done && n > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_validate_fide, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, out, done, seq);
   return hipGetLastError();
 }
 hipError_t launch_apply_fide(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
-                             uint8_t* info) {
+                             uint8_t* info, u32* done, u32 seq) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_apply_fide, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, verdicts, info);
+  if (done && n > 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_apply_fide, dim3(blocks_for(n, 256)), dim3(256), 0, st, pos, moves, n, verdicts, info, done, seq);
   return hipGetLastError();
 }
 hipError_t launch_replay_fide(hipStream_t st, const DevPos& start, const uint16_t* moves, u32 n_games, u32 n_plies,
