@@ -142,6 +142,33 @@ def test_validate_odd_pieces_and_oor(engine):
     assert (got == np.concatenate(want)).all()
 
 
+def test_validate_batch_sizes_across_paths(engine):
+    """Batch sizes either side of the pinned in-place path (<= 4096) and of its
+    host completion flag (<= 256), called back to back so every flag value is
+    fresh: verdicts equal the literal restatement's, and apply agrees."""
+    rng = np.random.default_rng(21)
+    ps = _positions(8, 21)
+    all_moves = np.array([f | (t << 6) for f in range(64) for t in range(64)], np.uint16)
+    pool_pos, pool_want = [], []
+    for p in ps:
+        for stm in (0, 1):
+            q = p.copy()
+            q.stm = stm
+            pool_pos.append(np.repeat(np.array([pos_of(q)], dchess.POS_DTYPE), 4096))
+            pool_want.append(O.ref_verdicts_all(q.cells, stm))
+    pool_pos = np.concatenate(pool_pos)
+    pool_mv = np.tile(all_moves, len(pool_want))
+    pool_want = np.concatenate(pool_want)
+    for n in (1, 2, 255, 256, 257, 1, 4096, 4097, 1, 9000, 256, 1):
+        idx = rng.choice(len(pool_mv), n, replace=False)
+        assert (engine.validate_batch(pool_pos[idx], pool_mv[idx]) == pool_want[idx]).all(), n
+        newpos, v, _ = engine.apply_batch(pool_pos[idx], pool_mv[idx])
+        assert (v == pool_want[idx]).all(), n
+        moved = v == 0  # accepted moves flip the side to move; rejected ones leave the position
+        assert (newpos["stm"][moved] != pool_pos[idx]["stm"][moved]).all()
+        assert (newpos[~moved] == pool_pos[idx][~moved]).all()
+
+
 def test_validate_empty_batch(engine):
     assert engine.validate_batch(np.zeros(0, dchess.POS_DTYPE), np.zeros(0, np.uint16)).size == 0
 
