@@ -1586,14 +1586,22 @@ hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const
   return hipGetLastError();
 }
 
+// k_count3c's special-child slots per parent and waves per SIMD (VGPR budget);
+// compile-time only (tools/ab_perft_libs.sh builds variants with -D).
+#ifndef DC_C3C_SLOTS
+#define DC_C3C_SLOTS 24
+#endif
+#ifndef DC_C3C_MINW
+#define DC_C3C_MINW 4
+#endif
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
                           const Range* rng_ch, const u32* mw, PerftResult* res) {
   if (stm_g) {
-    auto k = k_count3c<1, 256 * 24>;
+    auto k = k_count3c<1, 256 * DC_C3C_SLOTS, DC_C3C_MINW>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
                        res->divide, &res->next_chunk);
   } else {
-    auto k = k_count3c<0, 256 * 24>;
+    auto k = k_count3c<0, 256 * DC_C3C_SLOTS, DC_C3C_MINW>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
                        res->divide, &res->next_chunk);
   }
