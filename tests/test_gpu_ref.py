@@ -336,6 +336,16 @@ def test_perft_startpos_golden(engine, depth):
     assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
 
 
+def test_perft_repeated_runs_identical(engine):
+    """Repeated perfts of one position (plain runs, then graph replays) all
+    equal the golden: the final stage's block-level dynamic scheduling leaves
+    no run-to-run variation (round 2 saw a non-shipped LDS-layout variant of
+    c2c_group give varying perft(6) counts)."""
+    for depth in (5, 6, 7):
+        g = OG["perft_ref"]["startpos"][str(depth)]["total"]
+        assert [engine.perft(dchess.startpos(), depth)[0] for _ in range(5)] == [g] * 5
+
+
 def test_perft_random_positions_golden(engine):
     for e in OG["perft_ref"]["random_positions"]:
         d = dchess.pos_from_cells(np.array(e["cells"], np.int8), e["stm"])
