@@ -380,7 +380,8 @@ def test_perft_shards_sum(engine, n_shards, split):
     assert t == tot and (acc == div).all()
 
 
-@pytest.mark.parametrize("depth,n_shards,split", [(6, 3, 4), (7, 4, 4), (7, 3, 5), (6, 2, 3), (8, 2, 4)])
+@pytest.mark.parametrize("depth,n_shards,split", [(6, 3, 4), (7, 4, 4), (7, 3, 5), (6, 2, 3), (8, 2, 4), (7, 8, 3),
+                                                   (6, 8, 3)])
 def test_perft_deep_shards_golden(engine, depth, n_shards, split):
     """Strided shards cut after the top kernel (split 3), after k_make_count's
     level (4) or at the final stage's parents (5: k_count2c instead of
