@@ -899,9 +899,31 @@ __global__ __launch_bounds__(256, 4) void k_count2b(const Board* __restrict__ no
 // about 88 % of the children take the short path.
 constexpr int kC2cQueue = 128;
 
+#ifndef DC_C2C_SOA
+#define DC_C2C_SOA 0
+#endif
+// Parents' boards: array of structs (two ds_read_b128 per fetch, shipped);
+// DC_C2C_SOA=1 (A/B experiments only) keeps each bitboard in its own array.
+struct C2cParents {
+#if DC_C2C_SOA
+  u64 b[4][256];
+  __device__ __forceinline__ Board get(u32 i) const { return Board{b[0][i], b[1][i], b[2][i], b[3][i]}; }
+  __device__ __forceinline__ void set(u32 i, const Board& p) {
+    b[0][i] = p.b0;
+    b[1][i] = p.b1;
+    b[2][i] = p.b2;
+    b[3][i] = p.b3;
+  }
+#else
+  Board p[256];
+  __device__ __forceinline__ Board get(u32 i) const { return p[i]; }
+  __device__ __forceinline__ void set(u32 i, const Board& x) { p[i] = x; }
+#endif
+};
+
 template <u32 CAP>
 struct C2cShared {
-  Board par[256];
+  C2cParents par;
   u64 att[256];
   u32 base[256];
   u32 slot[CAP];
@@ -915,7 +937,7 @@ struct C2cShared {
 template <int STM, u32 CAP>
 __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
   const u32 pl = e >> 15;
-  Board ch = sh.par[pl];
+  Board ch = sh.par.get(pl);
   ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
   return ref_count<1 - STM>(ch);
 }
@@ -963,7 +985,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   u64 total64;
   const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
   const u32 total = (u32)total64;
-  sh.par[tid] = p;
+  sh.par.set(tid, p);
   sh.att[tid] = att;
   sh.base[tid] = base;
   sh.ptag[tid] = (uint16_t)tag;
@@ -988,7 +1010,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   };
   auto fetch = [&](u32 e) {
     const u32 pl = e >> 15;
-    return Cand{e, sh.base[pl], sh.par[pl], sh.att[pl]};
+    return Cand{e, sh.base[pl], sh.par.get(pl), sh.att[pl]};
   };
   auto consume = [&](const Cand& c, bool live) {
     const u32 pl = c.e >> 15;
