@@ -147,6 +147,7 @@ struct dc_ctx {
   DBuf<DevPos> pos;
   DBuf<uint16_t> moves;
   DBuf<uint8_t> verdicts, info;
+  DBuf<uint8_t> replay_info;  // dc_replay_info: ply-major [n_plies][n_games] move info
   DBuf<char> hash_text;    // escaped start history | escaped names of dc_state_hash*
   DBuf<u32> hash_off;      // the names' escaped offsets into hash_text
   DBuf<u32> esc_lens;      // device escaping scratch: per-name escaped lengths,
@@ -197,6 +198,7 @@ struct dc_ctx {
     pos.release();
     verdicts.release();
     info.release();
+    replay_info.release();
     hash_text.release();
     hash_off.release();
     esc_lens.release();
@@ -549,7 +551,7 @@ int dc_validate_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, const uint16
   if (n == 0) return DC_SUCCESS;
   if (n <= kHostIoBatch) {  // pinned, read in place by the kernel
     if (!c->host_io) {
-      HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo)));
+      HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo), hipHostMallocCoherent));
       c->host_io->done = 0;  // io_seq's values start at 1
     }
     HostIo* h = c->host_io;
@@ -588,7 +590,7 @@ int dc_apply_batch(dc_ctx* c, uint32_t rules, dc_pos* pos, const uint16_t* moves
   if (n == 0) return DC_SUCCESS;
   if (n <= kHostIoBatch) {  // pinned, read and written in place by the kernel
     if (!c->host_io) {
-      HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo)));
+      HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo), hipHostMallocCoherent));
       c->host_io->done = 0;  // io_seq's values start at 1
     }
     HostIo* h = c->host_io;
@@ -629,11 +631,15 @@ int dc_apply_batch(dc_ctx* c, uint32_t rules, dc_pos* pos, const uint16_t* moves
 
 // ================================================================== replay
 static int replay_impl(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* d_moves, uint32_t n_games,
-                       uint32_t n_plies, u64* d_bitmap, u64* d_digests, dc_replay_stats* stats) {
+                       uint32_t n_plies, u64* d_bitmap, u64* d_digests, dc_replay_stats* stats,
+                       uint8_t* d_info = nullptr) {
   dc_pos s;
   if (start) s = *start;
   else dc_startpos(&s);
   if (s.stm > 1) return DC_EINVAL;
+  // per-ply info: REF only (FIDE notation would need promotion/castling,
+  // which the reference's update_history never sees); one buffer descriptor
+  if (d_info && (rules != DC_RULES_REF || (u64)n_games * n_plies * 2 > 0xFFFFFFFFull)) return DC_EUNSUPPORTED;
   // stats5 = [5 totals | partials]; the reduction kernel writes all five totals
   HIP_TRY(c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(std::max<u32>(n_games, 1))));
   if (!c->replay_host) HIP_TRY(hipHostMalloc((void**)&c->replay_host, 5 * sizeof(u64)));
@@ -643,7 +649,7 @@ static int replay_impl(dc_ctx* c, uint32_t rules, const dc_pos* start, const uin
   HIP_TRY(c->timed("replay", (u64)n_games * n_plies, [&] {
     return rules == DC_RULES_REF
                ? dc::launch_replay_ref(c->stream, b, s.stm, d_moves, n_games, n_plies, d_bitmap, d_digests, c->stats5.p,
-                                       partial, c->replay_host, &host_written)
+                                       partial, c->replay_host, &host_written, d_info)
                : dc::launch_replay_fide(c->stream, reinterpret_cast<const DevPos&>(s), d_moves, n_games, n_plies,
                                         d_bitmap, d_digests, c->stats5.p, partial);
   }));
@@ -689,6 +695,38 @@ int dc_replay(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* mo
   int r = replay_impl(c, rules, start, c->moves.p, n_games, n_plies, bitmap ? c->bitmap.p : nullptr,
                       digests ? c->digests.p : nullptr, stats);
   if (r != DC_SUCCESS) return r;
+  if (bitmap && words)
+    HIP_TRY(hipMemcpyAsync(bitmap, c->bitmap.p, words * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  if (digests && n_games)
+    HIP_TRY(hipMemcpyAsync(digests, c->digests.p, (size_t)n_games * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
+  return sync_ctx(c);
+}
+
+int dc_replay_info_device(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* d_moves, uint32_t n_games,
+                          uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests, uint8_t* d_info,
+                          dc_replay_stats* stats) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n_games && n_plies && (!d_moves || !d_info))) return DC_EINVAL;
+  return replay_impl(c, rules, start, d_moves, n_games, n_plies, reinterpret_cast<u64*>(d_bitmap),
+                     reinterpret_cast<u64*>(d_digests), stats, d_info);
+}
+
+int dc_replay_info(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* moves, uint32_t n_games,
+                   uint32_t n_plies, uint64_t* bitmap, uint64_t* digests, uint8_t* info, dc_replay_stats* stats) {
+  ENTER(c);
+  if (rules > DC_RULES_FIDE || (n_games && n_plies && (!moves || !info))) return DC_EINVAL;
+  if (rules != DC_RULES_REF) return DC_EUNSUPPORTED;
+  const size_t nm = (size_t)n_games * n_plies;
+  const size_t words = (size_t)((n_games + 63) / 64) * n_plies;
+  HIP_TRY(c->moves.ensure(std::max<size_t>(nm, 1)));
+  HIP_TRY(c->replay_info.ensure(std::max<size_t>(nm, 1)));
+  if (bitmap) HIP_TRY(c->bitmap.ensure(std::max<size_t>(words, 1)));
+  if (digests) HIP_TRY(c->digests.ensure(std::max<size_t>(n_games, 1)));
+  if (nm) HIP_TRY(hipMemcpyAsync(c->moves.p, moves, nm * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  int r = replay_impl(c, rules, start, c->moves.p, n_games, n_plies, bitmap ? c->bitmap.p : nullptr,
+                      digests ? c->digests.p : nullptr, stats, c->replay_info.p);
+  if (r != DC_SUCCESS) return r;
+  if (nm) HIP_TRY(hipMemcpyAsync(info, c->replay_info.p, nm, hipMemcpyDeviceToHost, c->stream));
   if (bitmap && words)
     HIP_TRY(hipMemcpyAsync(bitmap, c->bitmap.p, words * sizeof(u64), hipMemcpyDeviceToHost, c->stream));
   if (digests && n_games)
@@ -818,6 +856,40 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
 }  // namespace
 
 extern "C" {
+
+// update_history (chess.rs:127-184) for one game's accepted plies, on the
+// host: the reference's notation (convert_move_to_notation, :134-154) with its
+// numbering quirk -- the move number is 1 + the number of whitespace-separated
+// tokens already in the history (:169-183), so it runs 1, 3, 5, ... from "".
+int dc_history_append(const char* history, const uint16_t* moves, const uint8_t* info, uint32_t n_plies,
+                      size_t stride, char* out, size_t out_cap, size_t* out_len) {
+  if ((n_plies && (!moves || !info)) || !out_len || (out_cap && !out)) return DC_EINVAL;
+  if (stride == 0) stride = 1;
+  std::string h = history ? history : "";
+  size_t tokens = count_ws_tokens(h.c_str(), h.size());  // split_whitespace().count()
+  static const char* kKind[7] = {"", "N", "B", "R", "Q", "K", ""};
+  for (uint32_t p = 0; p < n_plies; ++p) {
+    const uint8_t code = info[(size_t)p * stride];
+    const uint16_t m = moves[(size_t)p * stride];
+    if (code == 0xFF) continue;  // rejected or padded: not applied, no history entry
+    if ((code & 7) > 5) return DC_EUNSUPPORTED;  // an OTHER piece never moves (chess.rs:210)
+    const int f = m & 63, t = (m >> 6) & 63;
+    std::string san = kKind[code & 7];
+    if (code & 8) {
+      if ((code & 7) == 0) san += (char)('a' + (f & 7));
+      san += 'x';
+    }
+    san += (char)('a' + (t & 7));
+    san += std::to_string((t >> 3) + 1);
+    h += (tokens == 0 ? "" : " ") + std::to_string(tokens + 1) + ". " + san;
+    tokens += 2;
+  }
+  *out_len = h.size();
+  if (out_cap < h.size() + 1) return out_cap ? DC_EINVAL : DC_SUCCESS;
+  std::memcpy(out, h.c_str(), h.size() + 1);
+  return DC_SUCCESS;
+}
+
 
 int dc_keccak256(const void* data, size_t len, uint8_t out[32]) {
   if ((!data && len) || !out) return DC_EINVAL;

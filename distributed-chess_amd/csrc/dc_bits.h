@@ -31,11 +31,31 @@ constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
 // so one 64-bit shift (4 cycles per wave) beats the compiler's habit of
 // splitting it into v_alignbit_b32 + v_lshlrev_b32 once the halves feed
 // 32-bit bitop3s (tools/ubench/vop_rate.hip, profiles/r01/ubench_vop.txt).
+// DC_SHIFT_PAD (A/B diagnostics only): 1 = s_nop 1 ahead of the shift inside
+// the statement, 2 = s_nop 1 after it, 3 = plain C shifts (no asm).
+#ifndef DC_SHIFT_PAD
+#define DC_SHIFT_PAD 0
+#endif
+#if DC_SHIFT_PAD == 1
+#define DC_SHL_ASM "s_nop 1\n\tv_lshlrev_b64 %0, %1, %2"
+#define DC_SHR_ASM "s_nop 1\n\tv_lshrrev_b64 %0, %1, %2"
+#elif DC_SHIFT_PAD == 2
+#define DC_SHL_ASM "v_lshlrev_b64 %0, %1, %2\n\ts_nop 1"
+#define DC_SHR_ASM "v_lshrrev_b64 %0, %1, %2\n\ts_nop 1"
+#else
+#define DC_SHL_ASM "v_lshlrev_b64 %0, %1, %2"
+#define DC_SHR_ASM "v_lshrrev_b64 %0, %1, %2"
+#endif
 template <int S>
 __device__ __forceinline__ u64 sh(u64 x) {
   u64 r;
-  if constexpr (S > 0) asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(S), "v"(x));
-  else if constexpr (S < 0) asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(-S), "v"(x));
+#if DC_SHIFT_PAD == 3
+  if constexpr (S > 0) r = x << S;
+  else if constexpr (S < 0) r = x >> -S;
+#else
+  if constexpr (S > 0) asm(DC_SHL_ASM : "=v"(r) : "i"(S), "v"(x));
+  else if constexpr (S < 0) asm(DC_SHR_ASM : "=v"(r) : "i"(-S), "v"(x));
+#endif
   else r = x;
   return r;
 }

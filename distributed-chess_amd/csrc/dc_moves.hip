@@ -17,11 +17,14 @@ namespace dc {
 // HostIo): once the block's results are stored, thread 0 publishes seq to the
 // host flag with a system-scope release, so the caller can spin on the flag
 // instead of synchronising the stream (the live n = 1 consensus call).
+// Every thread makes its own stores visible at system scope before the
+// barrier (a fence orders only the issuing wave's stores, and up to four
+// waves write results), so the flag cannot overtake any wave's verdicts.
 __device__ __forceinline__ void publish_done(u32* done, u32 seq) {
   if (!done) return;
+  __threadfence_system();
   __syncthreads();
   if (threadIdx.x == 0) {  // a divergent (vector) store
-    __threadfence_system();
     __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -413,10 +416,15 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref3(Mailbox mb0, u64 occ
 //     p's mailbox reads, so only the (conflict-free) mailbox round trip is on
 //     a ply's dependency chain; the random, bank-conflicted table gathers
 //     overlap the previous ply's logic.
-template <int LOOK, int PF, bool DW>
+// INFO (dc_replay_info, the resync path): per ply and game one byte, the
+// moved piece's cell kind | 8 if the target held a piece (dc_apply_batch's
+// info, what update_history needs, chess.rs:156-167), 0xFF for a rejected ply;
+// ply-major like the moves.  Compiled out of the plain replay.
+template <int LOOK, int PF, bool DW, bool INFO = false>
 __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ0, u32 stm0, const uint16_t* __restrict__ moves,
                                                            u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
-                                                           u64* __restrict__ digests, u64* __restrict__ partial) {
+                                                           u64* __restrict__ digests, u64* __restrict__ partial,
+                                                           uint8_t* __restrict__ info = nullptr) {
   __shared__ __attribute__((aligned(16))) unsigned char r4_smem[kR3TabBytes + kR3MbBytes];
   u64* btw = reinterpret_cast<u64*>(r4_smem);
   u32* mb = reinterpret_cast<u32*>(r4_smem + kR3TabBytes);
@@ -477,7 +485,7 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
     // exit; their reads issue after ply p's mailbox reads, which LDS returns
     // first (in order), so the wait for the mailbox never waits on them
     Tab nx{0, 0};
-    auto ply_step = [&](u32 m, u32 slot, u32 mnext) {
+    auto ply_step = [&](u32 m, u32 slot, u32 mnext, u32 p) {
       const u32 m2 = m << 2, m3 = m << 3;
       const u32 af = __builtin_amdgcn_bitop3_b32(m << 9, tid4, 0x7000u, 0xE4);
       const u32 at = __builtin_amdgcn_bitop3_b32(m3, tid4, 0x7000u, 0xE4);
@@ -509,6 +517,12 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
                    : "+v"(bw_lo), "+v"(bw_hi)
                    : "s"((u32)w), "s"((u32)(w >> 32)), "s"(slot)
                    : "m0");
+      if constexpr (INFO) {
+        // cell kind by kind code (P0 N1 B2 R3 Q4 K5 X6; code 0 never moves)
+        constexpr u32 kCellKind = (0u << 4) | (1u << 8) | (5u << 12) | (6u << 16) | (2u << 20) | (3u << 24) | (4u << 28);
+        const u32 code = __builtin_amdgcn_ubfe(kCellKind, (nib >> 1) << 2, 4) | (nibt ? 8u : 0u);
+        if (active) info[(size_t)p * n_games + g] = (uint8_t)(ok ? code : 0xFFu);
+      }
       if (ok) {
         atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + af), nib << m2);
         atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + at), (nib ^ nibt) << st);
@@ -534,13 +548,13 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
       for (int k = 0; k < PF; ++k) {
         const u32 m = move_of(buf[k]);
         buf[k] = load_move(ply + PF + k);
-        ply_step(m, s0 + k, LOOK ? move_of(buf[(k + 1) % PF]) : 0u);  // k = PF - 1: ply + PF, reloaded at k = 0
+        ply_step(m, s0 + k, LOOK ? move_of(buf[(k + 1) % PF]) : 0u, ply + k);  // k = PF - 1: ply + PF, reloaded at k = 0
       }
       if (((ply + PF) & 63) == 0) flush(ply + PF - 64, 64);
     }
 #pragma unroll
     for (int k = 0; k < PF - 1; ++k)
-      if (ply + k < n_plies) ply_step(move_of(buf[k]), (ply + k) & 63, LOOK ? move_of(buf[k + 1]) : 0u);
+      if (ply + k < n_plies) ply_step(move_of(buf[k]), (ply + k) & 63, LOOK ? move_of(buf[k + 1]) : 0u, ply + k);
     if ((n_plies & 63) != 0) flush(n_plies & ~63u, n_plies & 63);
     accepted += nacc;  // a wave-level count: only the block sum is used
     if (lane == 0) validated += nvalw;  // wave-level count, added once per wave
@@ -874,9 +888,20 @@ static Mailbox host_mailbox(const Board& b) {
 
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                              u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial, u64* stats_host,
-                             bool* host_written) {
+                             bool* host_written, uint8_t* info) {
   *host_written = false;
   if (n_games == 0) return hipSuccess;
+  if (info && n_plies > 0) {  // the resync path: k_replay_ref4<.., INFO> (one buffer descriptor: < 4 GiB of moves)
+    if ((u64)n_games * n_plies * 2 > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const u32 nb = replay3_grid(n_games);
+    const bool dw = (n_games & 1) == 0;
+    auto ki = dw ? k_replay_ref4<0, 4, true, true> : k_replay_ref4<0, 4, false, true>;
+    hipLaunchKernelGGL(ki, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start), start.b1 | start.b2 | start.b3,
+                       stm0, moves, n_games, n_plies, bitmap, digests, partial, info);
+    hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats, stats_host);
+    *host_written = stats_host != nullptr;
+    return hipGetLastError();
+  }
   // n_plies == 0 (no moves buffer to clamp loads into) takes k_replay_ref
   if (n_plies > 0 && !replay_arith()) {
     const u32 nb = replay3_grid(n_games);
@@ -898,9 +923,12 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
     if (v4 == 41) k4 = dw ? k_replay_ref4<1, 4, true> : k_replay_ref4<1, 4, false>;
     if (v4 == 48) k4 = dw ? k_replay_ref4<0, 8, true> : k_replay_ref4<0, 8, false>;
     const bool fits = (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull;
-    hipLaunchKernelGGL((fits && !force3) ? k4 : k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st,
-                       host_mailbox(start), start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap,
-                       digests, partial);
+    if (fits && !force3)
+      hipLaunchKernelGGL(k4, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start), start.b1 | start.b2 | start.b3,
+                         stm0, moves, n_games, n_plies, bitmap, digests, partial, nullptr);
+    else
+      hipLaunchKernelGGL(k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start),
+                         start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap, digests, partial);
     hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats, stats_host);
     *host_written = stats_host != nullptr;
     return hipGetLastError();

@@ -902,6 +902,9 @@ constexpr int kC2cQueue = 128;
 #ifndef DC_C2C_SOA
 #define DC_C2C_SOA 0
 #endif
+#ifndef DC_C3C_STATIC
+#define DC_C3C_STATIC 0
+#endif
 // Parents' boards: array of structs (two ds_read_b128 per fetch, shipped);
 // DC_C2C_SOA=1 (A/B experiments only) keeps each bitboard in its own array.
 struct C2cParents {
@@ -1199,6 +1202,17 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
 // per grandparent enumerating into LDS while the block waited -- made the
 // final stage 0.56 vs 0.49 + 0.04 ms.)
 constexpr u32 kGroup = 256;
+#ifndef DC_C3C_LOG
+#define DC_C3C_LOG 0
+#endif
+#if DC_C3C_LOG
+constexpr u32 kC3cLogGroups = 20480, kC3cLogWords = 258;
+__device__ u64 g_c3c_log[kC3cLogGroups * kC3cLogWords];
+extern "C" __attribute__((visibility("default"))) int dc_ab_c3c_log(u64* out, u64 n_words) {
+  const u64 n = n_words < (u64)kC3cLogGroups * kC3cLogWords ? n_words : (u64)kC3cLogGroups * kC3cLogWords;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c3c_log), n * sizeof(u64), 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 constexpr u32 kMoveWordNodes = 1u << 20;  // grandparent index field of a move word
 
 // A level of more than kMoveWordNodes grandparents (possible only past a
@@ -1215,11 +1229,18 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
   const u32 tid = threadIdx.x;
   const u64 lo = rng->lo;
   const u32 total = (u32)(rng_ch->hi - rng_ch->lo);  // children (< 2^32: launcher)
+#if DC_C3C_STATIC
+  u32 k_static = 0;  // A/B diagnostics: block b takes groups b, b + grid, ... (no counter)
+#endif
   for (;;) {
     // (fetching the next group's index one group ahead, to take its round
     // trip off the load chain, made the kernel 0.495 -> 0.519 ms at perft(7):
     // a block then holds a group it cannot start, which lengthens the tail)
+#if DC_C3C_STATIC
+    if (tid == 0) sh.next = blockIdx.x + (k_static++) * gridDim.x;
+#else
     if (tid == 0) sh.next = atomicAdd(next_group, 1u);
+#endif
     __syncthreads();
     const u64 s = (u64)sh.next * kGroup;
     if (s >= total) break;  // block-uniform
@@ -1235,6 +1256,19 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
       ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
     }
     c2c_group<1 - STM_G, CAP>(sh, valid, ch, tag, divide);
+#if DC_C3C_LOG
+    // diagnostics: the block's cumulative histogram after each group
+    // (read back by dc_ab_c3c_log; tools/c2c_groups.py takes differences)
+    if (sh.next < kC3cLogGroups) {
+      u64* rec = g_c3c_log + (u64)sh.next * kC3cLogWords;
+      rec[tid] = sh.hist[tid];
+      if (tid == 0) {
+        rec[256] = blockIdx.x;
+        rec[257] = wall_clock64();
+      }
+    }
+    __syncthreads();
+#endif
   }
   tag_hist_flush(sh.hist, divide);
 }

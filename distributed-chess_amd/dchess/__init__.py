@@ -83,6 +83,12 @@ def lib():
         "dc_replay": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, C.POINTER(_Stats)]),
         "dc_replay_device": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp,
                                        C.POINTER(_Stats)]),
+        "dc_replay_info": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, _vp,
+                                     C.POINTER(_Stats)]),
+        "dc_replay_info_device": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, _vp,
+                                            C.POINTER(_Stats)]),
+        "dc_history_append": (C.c_int, [C.c_char_p, _vp, _vp, C.c_uint32, C.c_size_t, _vp, C.c_size_t,
+                                        C.POINTER(C.c_size_t)]),
         "dc_gen_games": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
                                    _vp]),
         "dc_gen_games_device": (C.c_int, [_vp, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
@@ -112,6 +118,22 @@ def lib():
         f.restype, f.argtypes = res, args
     _LIB = L
     return L
+
+
+def history_append(history, moves, info):
+    """dc_history_append: update_history (chess.rs:127-184) over one game's
+    plies (moves/info 1-D, one entry per ply).  Returns the new history."""
+    moves = np.ascontiguousarray(moves, np.uint16)
+    info = np.ascontiguousarray(info, np.uint8)
+    assert moves.shape == info.shape and moves.ndim == 1
+    n = C.c_size_t()
+    h = history.encode() if history is not None else None
+    _check(lib().dc_history_append(h, _ptr(moves), _ptr(info), len(moves), 1, None, 0, C.byref(n)),
+           "dc_history_append")
+    buf = C.create_string_buffer(n.value + 1)
+    _check(lib().dc_history_append(h, _ptr(moves), _ptr(info), len(moves), 1, buf, n.value + 1, C.byref(n)),
+           "dc_history_append")
+    return buf.value.decode()
 
 
 def exported_symbols():
@@ -364,6 +386,21 @@ class Engine:
                                _ptr(bitmap), _ptr(dig), C.byref(st)), "dc_replay")
         return bitmap, dig, {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
 
+    def replay_info(self, moves, start=None, want_bitmap=True, want_digests=True):
+        """dc_replay_info (RULES_REF): replay plus per-ply move info.  Returns
+        (bitmap, digests, info uint8 [n_plies, n_games], stats dict)."""
+        moves = np.ascontiguousarray(moves, np.uint16)
+        n_plies, n_games = moves.shape
+        words = (n_games + 63) // 64
+        bitmap = np.zeros((n_plies, words), np.uint64) if want_bitmap else None
+        dig = np.zeros(n_games, np.uint64) if want_digests else None
+        info = np.zeros((n_plies, n_games), np.uint8)
+        st = _Stats()
+        sp = np.array([start], POS_DTYPE) if start is not None else None
+        _check(lib().dc_replay_info(self.ctx, RULES_REF, _ptr(sp), _ptr(moves), n_games, n_plies, _ptr(bitmap),
+                                    _ptr(dig), _ptr(info), C.byref(st)), "dc_replay_info")
+        return bitmap, dig, info, {k: int(getattr(st, k)) for k, _ in _Stats._fields_}
+
     def replay_device(self, d_moves, n_games, n_plies, d_bitmap=None, d_digests=None, rules=RULES_REF):
         """d_* are DeviceBuffers or raw device addresses (e.g. a torch tensor's
         data_ptr(), for buffers that a torch.distributed collective reads)."""
@@ -605,11 +642,6 @@ class GameState:
         self.turn = turn
 
     def _update_history(self, frm, to, kind, capture):  # chess.rs:127-184 (GPU supplies kind/capture)
-        san = "" if kind == "P" else kind
-        if capture:
-            if kind == "P":
-                san += chr(ord("a") + frm.y)
-            san += "x"
-        san += chr(ord("a") + to.y) + str(to.x + 1)
-        n = len(self.history.split())
-        self.history += ("" if n == 0 else " ") + f"{n + 1}. {san}"
+        code = "PNBRQK".index(kind) | (8 if capture else 0)
+        self.history = history_append(self.history, np.array([move_pack(frm.x, frm.y, to.x, to.y)], np.uint16),
+                                      np.array([code], np.uint8))

@@ -99,6 +99,7 @@ class Replica:
         self.latest_block_hash = ZERO_HASH
         self.state_votes = {}    # block hash -> set of peer ids
         self.committed = []      # block hashes, in commit order
+        self.blocks = []         # the committed blocks themselves (a rejoining peer's resync source)
         self.rejections = []     # (where, reason)
         self.validate_calls = 0
         bus.replicas.append(self)
@@ -106,7 +107,7 @@ class Replica:
     # ------------------------------------------------------------ helpers
     def leader(self):
         peers = sorted(r.peer_id for r in self.bus.replicas)
-        return peers[self.view_n % PEERS]                       # hotstuff.rs:20-29
+        return peers[self.view_n % len(peers)]                  # hotstuff.rs:20-29 (PEERS = cluster size)
 
     @staticmethod
     def key(tx):
@@ -227,7 +228,7 @@ class Replica:
     def handle_commitment(self, commit):                       # p2p.rs:240-274
         b = commit["block"]
         votes = self.state_votes.get(b["hash"], set())
-        if self.view_n == b["view_n"] and _threshold_ok(len(votes)):
+        if self.view_n == b["view_n"] and _threshold_ok(len(votes), len(self.bus.replicas)):
             b = dict(b, qc={"block_hash": b["hash"], "signature": sorted(votes)})
             self.bus.publish("commit", self.peer_id, b)
             self.view_n = b["view_n"] + 1
@@ -243,7 +244,7 @@ class Replica:
         if qc is None:
             return self.rejections.append(("commit", "invalid qc"))
         votes = self.state_votes.get(qc["block_hash"], set())  # is_valid_qc, hotstuff.rs:210-223
-        if not _threshold_ok(len(votes & set(qc["signature"]))):
+        if not _threshold_ok(len(votes & set(qc["signature"])), len(self.bus.replicas)):
             return self.rejections.append(("commit", "invalid qc"))
         k = self.key(block["tx"])
         g = self.db.get(k)
@@ -263,6 +264,35 @@ class Replica:
             raise AssertionError(f"{self.peer_id}: dc_state_hash disagrees with the GameState mirror")
         self.latest_block_hash = block["hash"]
         self.committed.append(block["hash"])
+        self.blocks.append(block)
+
+
+def resync_game(engine, blocks, history=""):
+    """A replica that missed a game's commits rebuilds it from the committed
+    blocks (in commit order) in one GPU replay instead of commit_block's
+    per-block apply_move + update_history (hotstuff.rs:41-56): dc_replay_info
+    replays the blocks' moves and reports each ply's moved kind and capture
+    flag, dc_history_append turns them into update_history's text
+    (chess.rs:127-184), and every block's hash -- BlockBuilder over the
+    history BEFORE its move (types.rs:45-55, built in commit_block
+    hotstuff.rs:41-46) -- is checked against the rebuilt prefix.
+    Returns (final history, the moves as uint16, the first block index whose
+    hash or verdict disagrees or None)."""
+    mv = np.array([dchess.move_pack(b["tx"]["action"][0]["x"], b["tx"]["action"][0]["y"],
+                                    b["tx"]["action"][1]["x"], b["tx"]["action"][1]["y"]) for b in blocks],
+                  np.uint16)
+    if len(mv) == 0:
+        return history, mv, None
+    _, _, info, st = engine.replay_info(mv.reshape(-1, 1), want_bitmap=False, want_digests=False)
+    info = info[:, 0]
+    before = history
+    for i, b in enumerate(blocks):
+        if info[i] == 0xFF:      # a committed block's move must be legal in the replayed game
+            return before, mv, i
+        if block_hash(b["view_n"], b["previous_block_hash"], before, b["tx"]) != b["hash"]:
+            return before, mv, i
+        before = dchess.history_append(before, mv[i:i + 1], info[i:i + 1])
+    return before, mv, None
 
 
 def make_cluster(n=PEERS, check_signatures=True, engine_factory=None):

@@ -141,26 +141,15 @@ std::optional<AppError> GameState::apply_move(Engine& e, const Position& from, c
   uint8_t v = 0, info = 0;
   check(dc_apply_batch(e.ctx(), DC_RULES_REF, &p, &m, 1, &v, &info), "dc_apply_batch");
   if (auto err = verdict_to_result(v)) return err;  // rejected: state untouched (chess.rs:44-46)
-  // update_history (chess.rs:156-184) from the kernel's mover kind / capture flag
-  const Piece mover = *board[from.x][from.y];
-  const bool capture = (info & 8) != 0;
-  std::string san = mover.kind == "P" ? "" : mover.kind;
-  if (capture) {
-    if (mover.kind == "P") san.push_back(static_cast<char>('a' + from.y));
-    san.push_back('x');
-  }
-  san.push_back(static_cast<char>('a' + to.y));
-  san += std::to_string(to.x + 1);
+  // update_history (chess.rs:156-184) from the kernel's mover kind / capture
+  // flag, formatted by the ABI's dc_history_append (split_whitespace numbering)
   std::string& h = *history;
-  size_t tokens = 0;
-  bool in_tok = false;
-  for (char ch : h) {
-    const bool ws = ch == ' ' || ch == '\t' || ch == '\n';
-    if (!ws && !in_tok) ++tokens;
-    in_tok = !ws;
-  }
-  if (tokens) h.push_back(' ');
-  h += std::to_string(tokens + 1) + ". " + san;
+  size_t len = 0;
+  check(dc_history_append(h.c_str(), &m, &info, 1, 1, nullptr, 0, &len), "dc_history_append");
+  std::string out(len + 1, '\0');
+  check(dc_history_append(h.c_str(), &m, &info, 1, 1, out.data(), out.size(), &len), "dc_history_append");
+  out.resize(len);
+  h = out;
   // the board after the move, from the kernel's position (unknown kinds never move)
   int8_t cells[64];
   uint8_t t = 0;

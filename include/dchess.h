@@ -177,6 +177,30 @@ int dc_replay_device(dc_ctx* ctx, uint32_t rules, const dc_pos* start, const uin
                      uint32_t n_games, uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests,
                      dc_replay_stats* stats);
 
+/* Replay for a resyncing replica (the history-rebuild path): dc_replay plus
+ * info (ply-major [n_plies][n_games] bytes, like the moves): for an accepted
+ * ply the moved piece's cell kind (0 P .. 5 K) | 8 if the target held a piece
+ * -- dc_apply_batch's info, what update_history needs (chess.rs:156-167) --
+ * and 0xFF for a rejected or DC_MOVE_NONE ply.  RULES_REF only (else
+ * DC_EUNSUPPORTED), and n_games * n_plies * 2 < 4 GiB per call.
+ * Replaces commit_block's per-move apply_move + update_history loop
+ * (core/src/consensus/hotstuff.rs:41-56) for a whole move log at once. */
+int dc_replay_info(dc_ctx* ctx, uint32_t rules, const dc_pos* start, const uint16_t* moves, uint32_t n_games,
+                   uint32_t n_plies, uint64_t* bitmap, uint64_t* digests, uint8_t* info, dc_replay_stats* stats);
+int dc_replay_info_device(dc_ctx* ctx, uint32_t rules, const dc_pos* start, const uint16_t* d_moves,
+                          uint32_t n_games, uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests,
+                          uint8_t* d_info, dc_replay_stats* stats);
+/* GameState::update_history (chess.rs:127-184) over one game's plies, on the
+ * host: history (NUL-terminated UTF-8, NULL = "") followed by one
+ * "N. <notation>" token pair per accepted ply (info != 0xFF), numbered as the
+ * reference numbers them (N = 1 + the whitespace-separated tokens already
+ * present: 1, 3, 5, ...).  moves/info of ply p at [p * stride] (stride =
+ * n_games for a column of dc_replay_info's ply-major arrays).  *out_len = the
+ * result's length; out (capacity out_cap, incl. the NUL) receives it, or
+ * DC_EINVAL if out_cap is too small (out_cap = 0 only sizes it). */
+int dc_history_append(const char* history, const uint16_t* moves, const uint8_t* info, uint32_t n_plies,
+                      size_t stride, char* out, size_t out_cap, size_t* out_len);
+
 /* Seeded synthetic games: rng = splitmix64 from seed ^ game_id;
  * per ply one draw r: (r & 0xFF) < noise_per_256 -> move (r>>8)&0xFFF, else the
  * ((r>>32)*n>>32)-th legal move in (from, to, promo) order; no legal move ->

@@ -199,10 +199,26 @@ void GameState::update_history(const Position& from, const Position& to) {
   const Piece& mover = *board->rows[from.x].cells[from.y].piece;
   const bool capture = board->rows[to.x].cells[to.y].piece.has_value();
   std::string san = notation(from, to, mover, capture);
-  std::istringstream in(*history);
+  // chess.rs:169-175: history.split_whitespace().count() -- Rust's
+  // char::is_whitespace, i.e. the Unicode White_Space set, over UTF-8 text
+  // (an ASCII-only split would miss e.g. U+3000 or U+00A0 in a name-bearing
+  // start history)
+  auto white = [](uint32_t c) {
+    return (c >= 0x09 && c <= 0x0D) || c == 0x20 || c == 0x85 || c == 0xA0 || c == 0x1680 ||
+           (c >= 0x2000 && c <= 0x200A) || c == 0x2028 || c == 0x2029 || c == 0x202F || c == 0x205F || c == 0x3000;
+  };
   size_t n = 0;
-  std::string tok;
-  while (in >> tok) ++n;
+  bool in_word = false;
+  const std::string& hs = *history;
+  for (size_t i = 0; i < hs.size();) {
+    const unsigned char c0 = (unsigned char)hs[i];
+    const int len = c0 < 0x80 ? 1 : c0 < 0xE0 ? 2 : c0 < 0xF0 ? 3 : 4;
+    uint32_t c = len == 1 ? c0 : len == 2 ? (c0 & 0x1F) : len == 3 ? (c0 & 0x0F) : (c0 & 0x07);
+    for (int k = 1; k < len && i + k < hs.size(); ++k) c = (c << 6) | ((unsigned char)hs[i + k] & 0x3F);
+    i += len;
+    if (white(c)) in_word = false;
+    else if (!in_word) { in_word = true; ++n; }
+  }
   std::string& h = *history;
   if (n != 0) h.push_back(' ');
   h += std::to_string(n + 1);

@@ -147,3 +147,32 @@ def test_quorum_threshold_with_silent_replicas(engines):
         assert leader.transact(signed_tx(1, 4, 3, 4, 0))
         bus.run()
         assert bool(leader.committed) == commits, silent
+
+
+def test_rejoining_replica_resyncs_history_and_block_hashes(engines):
+    """Resync path: after the scripted game commits, a fresh
+    dc_ctx rebuilds the game from the leader's committed blocks with one
+    dc_replay_info + dc_history_append and reproduces every block hash
+    (types.rs:45-55 over the history before each move), the final history and
+    the final game-state hash; a tampered block is caught at its index."""
+    g = OG["replica_game"]
+    bus, reps = cluster(engines)
+    turn = 0
+    for ply, (fx, fy, tx_, ty) in enumerate(g["moves"]):
+        if reps[ply % R.PEERS].transact(signed_tx(fx, fy, tx_, ty, turn)):
+            turn ^= 1
+        bus.run()
+    blocks = reps[0].blocks
+    assert len(blocks) == sum(v == 0 for v in g["verdicts"]) > 0
+    fresh = dchess.Engine(0)
+    try:
+        hist, mv, bad = R.resync_game(fresh, blocks)
+        assert bad is None and hist == g["history"]
+        k = f"{WHITE}:{BLACK}"
+        h = fresh.state_hash(mv.reshape(-1, 1), [(WHITE, BLACK)])[0]
+        assert "0x" + bytes(h).hex() == reps[0].game_state_hash(k)
+        forged = [dict(b) for b in blocks]
+        forged[3] = dict(forged[3], view_n=forged[3]["view_n"] + 1)
+        assert R.resync_game(fresh, forged)[2] == 3
+    finally:
+        fresh.close()
