@@ -23,20 +23,62 @@ def test_library_exports_every_header_symbol():
         assert hasattr(L, n), n
 
 
+_C2RS = {"int": "c_int", "uint8_t": "u8", "int8_t": "i8", "uint16_t": "u16", "uint32_t": "u32",
+         "uint64_t": "u64", "size_t": "usize", "char": "c_char", "void": "c_void", "dc_ctx": "dc_ctx",
+         "dc_pos": "dc_pos", "dc_replay_stats": "dc_replay_stats", "dc_kernel_stats": "dc_kernel_stats"}
+
+
+def _c_to_rust(t):
+    """C parameter/return type (name stripped) -> the Rust FFI type it must be."""
+    t = " ".join(t.split())
+    arr = t.endswith("]")
+    if arr:  # `const int8_t cells[64]` decays to a pointer
+        t = t[:t.index("[")].rsplit(" ", 1)[0] + " *"
+    stars = t.count("*")
+    base = t.replace("*", " ").split()
+    const = base[0] == "const"
+    name = base[-1] if not const else base[1]
+    rs = _C2RS[name]
+    if stars == 0:
+        return rs
+    out = ("*const " if const else "*mut ") + rs
+    for _ in range(stars - 1):
+        out = "*mut " + out
+    return out
+
+
 def test_rust_binding_matches_header():
-    """integration/rust/src/lib.rs (unverified: no cargo here) declares only
-    symbols the header declares, with the same parameter count."""
+    """integration/rust/src/lib.rs (unverified: no cargo here) declares EVERY
+    function of include/dchess.h, each parameter and the return value with the
+    Rust type the C type maps to; and its safe layer has no panicking calls."""
     import re
-    hdr = open(os.path.join(os.path.dirname(dchess.LIB_PATH), "..", "include", "dchess.h")).read()
-    rs = open(os.path.join(os.path.dirname(dchess.LIB_PATH), "..", "integration", "rust", "src", "lib.rs")).read()
-    hdr_args = {m.group(1): len([a for a in m.group(2).split(",") if a.strip() not in ("", "void")])
-                for m in re.finditer(r"(dc_\w+)\s*\(([^)]*)\)\s*;", hdr)}
-    rs_fns = {m.group(1): len([a for a in m.group(2).split(",") if a.strip()])
-              for m in re.finditer(r"pub fn (dc_\w+)\(([^)]*)\)", rs)}
-    assert len(rs_fns) >= 15
-    for name, n in rs_fns.items():
-        assert name in hdr_args, name
-        assert hdr_args[name] == n, (name, hdr_args[name], n)
+    root = os.path.join(os.path.dirname(dchess.LIB_PATH), "..")
+    hdr = re.sub(r"/\*.*?\*/", "", open(os.path.join(root, "include", "dchess.h")).read(), flags=re.S)
+    rs = open(os.path.join(root, "integration", "rust", "src", "lib.rs")).read()
+    decls = {}
+    for m in re.finditer(r"^\s*((?:const\s+)?\w+\s*\**)\s*(dc_\w+)\s*\(([^)]*)\)\s*;", hdr, re.M):
+        ret, name, args = m.group(1), m.group(2), " ".join(m.group(3).split())
+        params = [] if args in ("", "void") else [a.strip() for a in args.split(",")]
+        types = []
+        for a in params:  # drop the parameter name (keep an array suffix)
+            mm = re.match(r"(.*?)(\w+)(\[\d+\])?$", a)
+            types.append(_c_to_rust(mm.group(1) + ("x" + mm.group(3) if mm.group(3) else "")).strip()
+                         if mm.group(3) else _c_to_rust(mm.group(1)))
+        decls[name] = (_c_to_rust(ret), types)
+    assert len(decls) >= 40
+    rs_fns = {}
+    for m in re.finditer(r"pub fn (dc_\w+)\(([^)]*)\)\s*(?:->\s*([^;]+))?;", rs):
+        args = [a.strip() for a in " ".join(m.group(2).split()).split(",") if a.strip()]
+        rs_fns[m.group(1)] = ((m.group(3) or "()").strip(), [a.split(":", 1)[1].strip() for a in args])
+    missing = sorted(set(decls) - set(rs_fns))
+    assert not missing, missing
+    for name, (ret, types) in decls.items():
+        rret, rtypes = rs_fns[name]
+        assert rret == ret, (name, rret, ret)
+        assert rtypes == types, (name, rtypes, types)
+    safe = rs[rs.index("pub struct DcError"):]
+    for bad in ("assert!(", "assert_eq!(", ".unwrap()", ".expect(", "panic!(", "unreachable!("):
+        assert bad not in safe, bad
 
 
 def test_version_and_messages():
