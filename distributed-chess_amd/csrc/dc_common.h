@@ -66,9 +66,9 @@ __device__ __forceinline__ void tag_hist_add(u64* hist, u32 tag, u64 v, bool val
     atomicAdd((unsigned long long*)&hist[tag], (unsigned long long)v);
   }
 }
-__device__ __forceinline__ void tag_hist_flush(const u64* hist, u64* divide) {
+__device__ __forceinline__ void tag_hist_flush(const u64* hist, u64* divide, u32 tid = threadIdx.x) {
   __syncthreads();
-  for (u32 t = threadIdx.x; t < 256; t += blockDim.x)
+  for (u32 t = tid; t < 256; t += blockDim.x)
     if (hist[t]) atomicAdd((unsigned long long*)(divide + t), (unsigned long long)hist[t]);
 }
 

@@ -77,9 +77,22 @@ __device__ __forceinline__ u32 count_rt(const Board& b, u32 meta, u32 stm) {
 
 // ------------------------------------------------------------- block scan
 // Exclusive scan over a 1024-thread (16-wave) or 256-thread block.
+// threadIdx.x rebuilt at the point of use from the lane's mbcnt and the
+// wave's index (an SGPR): an opaque statement the compiler cannot hoist or
+// merge, so no thread-index-derived address stays live (and spills) across
+// the final stage's register-heavy code (round 3: k_count3c spill-free).
+__device__ __forceinline__ u32 otid(u32 wave) {
+  u32 t;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshl_add_u32 %0, %1, 6, %0"
+               : "=&v"(t)
+               : "s"(wave));
+  return t;
+}
+
 template <int NW>
-__device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* wsum /*LDS[NW]*/, u64* total) {
-  const u32 lane = lane_id(), w = threadIdx.x >> 6;
+__device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* wsum /*LDS[NW]*/, u64* total,
+                                                 u32 w = threadIdx.x >> 6) {
+  const u32 lane = lane_id();
   const u64 incl = wave_incl_scan64(v);
   if (lane == 63) wsum[w] = incl;
   __syncthreads();
@@ -902,6 +915,9 @@ constexpr int kC2cQueue = 128;
 #ifndef DC_C2C_SOA
 #define DC_C2C_SOA 0
 #endif
+#ifndef DC_C2C_PAIR
+#define DC_C2C_PAIR 1
+#endif
 #ifndef DC_C3C_STATIC
 #define DC_C3C_STATIC 0
 #endif
@@ -924,23 +940,64 @@ struct C2cParents {
 #endif
 };
 
+#ifndef DC_C2C_REC
+#define DC_C2C_REC 0
+#endif
+// DC_C2C_REC = 1: each parent's board, rays, base count and tag in one 48-byte
+// record (one per-thread LDS address instead of four differently scaled ones).
+struct alignas(16) C2cRec {
+  u64 b0, b1, b2, b3, att;
+  u32 base;
+  uint16_t tag, pad;
+};
+// Special-child slots per group of 256 parents: 24 per parent, trimmed with
+// the 48-byte records so that four blocks' LDS (<= 40,960 B each) fit a CU.
+constexpr u32 kC2cCap = DC_C2C_REC ? 6128 : 256 * 24;
+
 template <u32 CAP>
 struct C2cShared {
+#if DC_C2C_REC
+  C2cRec rec[256];
+#else
   C2cParents par;
   u64 att[256];
   u32 base[256];
+#endif
   u32 slot[CAP];
   u32 queue[4][kC2cQueue];
   u64 hist[256];
   u64 wsum[4];
   u32 next;
+#if !DC_C2C_REC
   uint16_t ptag[256];
+#endif
+  __device__ __forceinline__ void put(u32 i, const Board& p, u64 a, u32 bs, u32 tg) {
+#if DC_C2C_REC
+    rec[i] = C2cRec{p.b0, p.b1, p.b2, p.b3, a, bs, (uint16_t)tg, 0};
+#else
+    par.set(i, p);
+    att[i] = a;
+    base[i] = bs;
+    ptag[i] = (uint16_t)tg;
+#endif
+  }
+#if DC_C2C_REC
+  __device__ __forceinline__ Board board(u32 i) const { return Board{rec[i].b0, rec[i].b1, rec[i].b2, rec[i].b3}; }
+  __device__ __forceinline__ u64 rays(u32 i) const { return rec[i].att; }
+  __device__ __forceinline__ u32 basec(u32 i) const { return rec[i].base; }
+  __device__ __forceinline__ u32 tag(u32 i) const { return rec[i].tag; }
+#else
+  __device__ __forceinline__ Board board(u32 i) const { return par.get(i); }
+  __device__ __forceinline__ u64 rays(u32 i) const { return att[i]; }
+  __device__ __forceinline__ u32 basec(u32 i) const { return base[i]; }
+  __device__ __forceinline__ u32 tag(u32 i) const { return ptag[i]; }
+#endif
 };
 
 template <int STM, u32 CAP>
 __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
   const u32 pl = e >> 15;
-  Board ch = sh.par.get(pl);
+  Board ch = sh.board(pl);
   ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
   return ref_count<1 - STM>(ch);
 }
@@ -963,8 +1020,10 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
 // a block barrier (par/att/ptag/slot are reused by the next group).
 template <int STM, u32 CAP, int PHASE = 0, bool BULK = true>
 __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const Board& p, u32 tag,
-                                          u64* __restrict__ divide) {
-  const u32 tid = threadIdx.x, w = tid >> 6, lane = lane_id();
+                                          u64* __restrict__ divide, u32 wave) {
+  // wave: this wave's index in the block (an SGPR, readfirstlane at kernel
+  // entry); the thread index is rebuilt where it is used (otid)
+  const u32 w = wave, lane = lane_id();
   u32* q = sh.queue[w];
   u32 cnt = 0, base = 0;
   u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
@@ -986,19 +1045,16 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     }
   }
   u64 total64;
-  const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
+  const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64, w);
   const u32 total = (u32)total64;
-  sh.par.set(tid, p);
-  sh.att[tid] = att;
-  sh.base[tid] = base;
-  sh.ptag[tid] = (uint16_t)tag;
+  sh.put(otid(w), p, att, base, tag);
   __syncthreads();
-  const u32 tag0 = sh.ptag[0];
+  const u32 tag0 = sh.tag(0);
   u64 acc = 0;  // grandchildren under parents whose tag == tag0
   auto add = [&](u32 pl, u32 k, bool live) {
     if constexpr (PHASE == 7) return;
     if (!live) return;
-    const u32 ptag = sh.ptag[pl];
+    const u32 ptag = sh.tag(pl);
     if (ptag == tag0) acc += k;
     else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
   };
@@ -1013,7 +1069,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   };
   auto fetch = [&](u32 e) {
     const u32 pl = e >> 15;
-    return Cand{e, sh.base[pl], sh.par.get(pl), sh.att[pl]};
+    return Cand{e, sh.basec(pl), sh.board(pl), sh.rays(pl)};
   };
   auto consume = [&](const Cand& c, bool live) {
     const u32 pl = c.e >> 15;
@@ -1061,7 +1117,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     if (lane + 64 < qn) q[lane] = q[lane + 64];
     qn = __builtin_amdgcn_readfirstlane(qn - 64);
   };
-  if constexpr (BULK && PHASE != 7) add(tid, (u32)simple_leaves, valid);
+  if constexpr (BULK && PHASE != 7) add(otid(w), (u32)simple_leaves, valid);
   if constexpr (PHASE == 7) {  // [2] simple children, [3] parents
     const u64 ns = wave_sum64(nsim), np = __popcll(ballot(valid));
     if (lane == 0) {
@@ -1077,14 +1133,15 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       if constexpr (BULK) ref_for_each_special<STM>(p, Fs, Ts, visit);
       else ref_for_each_move<STM>(p, visit);
     };
+    const u32 pl15 = otid(w) << 15;
     if (total <= CAP) {  // the norm: one window, no range checks
       u32 j = excl;
-      if (valid) each_move([&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | (tid << 15); });
+      if (valid) each_move([&](int f, int t) { sh.slot[j++] = (u32)f | ((u32)t << 6) | pl15; });
     } else {
       u32 j = excl;
       if (valid && j < wbase + CAP && j + cnt > wbase) {
         each_move([&](int f, int t) {
-          if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | (tid << 15);
+          if (j >= wbase && j - wbase < CAP) sh.slot[j - wbase] = (u32)f | ((u32)t << 6) | pl15;
           ++j;
         });
       }
@@ -1093,7 +1150,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     const u32 nslots = min(CAP, total - wbase);
     // two slots per lane per step, loaded together, so the LDS round trips overlap
     u32 r0 = (PHASE == 1 || PHASE == 2) ? nslots : w * 64;
-    for (; r0 + 256 < nslots; r0 += 512) {
+    for (; DC_C2C_PAIR && r0 + 256 < nslots; r0 += 512) {
       const u32 ra = r0 + lane, rb = r0 + 256 + lane;
       const bool lb = rb < nslots;
       const Cand ca = fetch(sh.slot[ra]);
@@ -1103,7 +1160,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       consume(cb, lb);
       if (qn >= 64) drain64();
     }
-    if (r0 < nslots) {
+    for (; r0 < nslots; r0 += 256) {  // (DC_C2C_PAIR: at most one round left)
       const u32 ra = r0 + lane;
       const bool la = ra < nslots;
       consume(fetch(la ? sh.slot[ra] : 0u), la);
@@ -1165,7 +1222,7 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
       p = load_board(nodes, i);
       tag = tags[i];
     }
-    c2c_group<STM, CAP, GP, BULK>(sh, valid, p, tag, divide);
+    c2c_group<STM, CAP, GP, BULK>(sh, valid, p, tag, divide, __builtin_amdgcn_readfirstlane(tid >> 6));
   }
   tag_hist_flush(sh.hist, divide);
 #ifdef DC_AB_KNOBS
@@ -1226,7 +1283,8 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
                                                  u32* __restrict__ next_group) {
   __shared__ C2cShared<CAP> sh;
   tag_hist_init(sh.hist);
-  const u32 tid = threadIdx.x;
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool t0 = wave == 0 && lane_id() == 0;
   const u64 lo = rng->lo;
   const u32 total = (u32)(rng_ch->hi - rng_ch->lo);  // children (< 2^32: launcher)
 #if DC_C3C_STATIC
@@ -1237,14 +1295,14 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
     // trip off the load chain, made the kernel 0.495 -> 0.519 ms at perft(7):
     // a block then holds a group it cannot start, which lengthens the tail)
 #if DC_C3C_STATIC
-    if (tid == 0) sh.next = blockIdx.x + (k_static++) * gridDim.x;
+    if (t0) sh.next = blockIdx.x + (k_static++) * gridDim.x;
 #else
-    if (tid == 0) sh.next = atomicAdd(next_group, 1u);
+    if (t0) sh.next = atomicAdd(next_group, 1u);
 #endif
     __syncthreads();
     const u64 s = (u64)sh.next * kGroup;
     if (s >= total) break;  // block-uniform
-    const u64 i = s + tid;
+    const u64 i = s + otid(wave);
     const bool valid = i < total;
     Board ch{0, 0, 0, 0};
     u32 tag = 0;
@@ -1255,12 +1313,13 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
       tag = tags[g];
       ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
     }
-    c2c_group<1 - STM_G, CAP>(sh, valid, ch, tag, divide);
+    c2c_group<1 - STM_G, CAP>(sh, valid, ch, tag, divide, wave);
 #if DC_C3C_LOG
     // diagnostics: the block's cumulative histogram after each group
     // (read back by dc_ab_c3c_log; tools/c2c_groups.py takes differences)
     if (sh.next < kC3cLogGroups) {
       u64* rec = g_c3c_log + (u64)sh.next * kC3cLogWords;
+      const u32 tid = otid(wave);
       rec[tid] = sh.hist[tid];
       if (tid == 0) {
         rec[256] = blockIdx.x;
@@ -1270,7 +1329,7 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
     __syncthreads();
 #endif
   }
-  tag_hist_flush(sh.hist, divide);
+  tag_hist_flush(sh.hist, divide, otid(wave));
 }
 
 // ------------------------------------------------- K4: per-lane DFS (REF)
@@ -1375,7 +1434,7 @@ __global__ __launch_bounds__(256, 3) void k_perft_dfs(const Board* __restrict__ 
       }
     }
     if (__syncthreads_or(valid) == 0) break;  // every lane of the block is done
-    c2c_group<STM_P, CAP>(sh, valid, p, tag, divide);
+    c2c_group<STM_P, CAP>(sh, valid, p, tag, divide, __builtin_amdgcn_readfirstlane(threadIdx.x >> 6));
   }
   tag_hist_flush(sh.hist, divide);
 }
@@ -1570,19 +1629,19 @@ static void launch_count2c(hipStream_t st, int stm, const Board* nodes, const ui
     return e ? std::atoi(e) : 4;
   }();
 #ifdef DC_AB_KNOBS
-  if (phase == 1) launch_count2c_cap<256 * 24, 1, true>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 2) launch_count2c_cap<256 * 24, 2, true>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 3) launch_count2c_cap<256 * 24, 0, false>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 5) launch_count2c_cap<256 * 24, 5, true>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 6) launch_count2c_cap<256 * 24, 6, true>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 7) launch_count2c_cap<256 * 24, 7, true>(st, stm, nodes, tags, rng, divide);
-  else if (phase == 8) launch_count2c_cap<256 * 24, 8, true>(st, stm, nodes, tags, rng, divide);
-  else if (waves == 4) launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
-  else launch_count2c_cap<256 * 24, 0, true, 3>(st, stm, nodes, tags, rng, divide);
+  if (phase == 1) launch_count2c_cap<kC2cCap, 1, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 2) launch_count2c_cap<kC2cCap, 2, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 3) launch_count2c_cap<kC2cCap, 0, false>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 5) launch_count2c_cap<kC2cCap, 5, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 6) launch_count2c_cap<kC2cCap, 6, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 7) launch_count2c_cap<kC2cCap, 7, true>(st, stm, nodes, tags, rng, divide);
+  else if (phase == 8) launch_count2c_cap<kC2cCap, 8, true>(st, stm, nodes, tags, rng, divide);
+  else if (waves == 4) launch_count2c_cap<kC2cCap, 0, true, 4>(st, stm, nodes, tags, rng, divide);
+  else launch_count2c_cap<kC2cCap, 0, true, 3>(st, stm, nodes, tags, rng, divide);
 #else
   (void)phase;
   (void)waves;
-  launch_count2c_cap<256 * 24, 0, true, 4>(st, stm, nodes, tags, rng, divide);
+  launch_count2c_cap<kC2cCap, 0, true, 4>(st, stm, nodes, tags, rng, divide);
 #endif
 }
 
@@ -1607,7 +1666,7 @@ extern "C" __attribute__((visibility("default"))) int dc_ab_top_trace(u64* out) 
 #endif
 
 u64 dfs_lanes() {
-  return (u64)resident_grid(k_perft_dfs<0, 256 * 24, 1>, 256, kMaxGrid) * 256;
+  return (u64)resident_grid(k_perft_dfs<0, kC2cCap, 1>, 256, kMaxGrid) * 256;
 }
 
 hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* nodes, const uint16_t* tags,
@@ -1615,7 +1674,7 @@ hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* 
   const DfsStack ds{stack_frames, lanes};
   const u32 grid = (u32)(lanes / 256);
 #define DC_DFS(S, LL)                                                                                        \
-  hipLaunchKernelGGL((k_perft_dfs<S, 256 * 24, LL>), dim3(grid), dim3(256), 0, st, nodes, tags, rng, res->divide, \
+  hipLaunchKernelGGL((k_perft_dfs<S, kC2cCap, LL>), dim3(grid), dim3(256), 0, st, nodes, tags, rng, res->divide, \
                      &res->dfs_next, ds)
   if (L == 1) {
     if (stm_parent) DC_DFS(1, 1);
@@ -1644,8 +1703,10 @@ hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const
 
 // k_count3c's special-child slots per parent and waves per SIMD (VGPR budget);
 // compile-time only (tools/ab_perft_libs.sh builds variants with -D).
-#ifndef DC_C3C_SLOTS
-#define DC_C3C_SLOTS 24
+#ifdef DC_C3C_SLOTS
+constexpr u32 kC3cCap = 256 * DC_C3C_SLOTS;
+#else
+constexpr u32 kC3cCap = kC2cCap;
 #endif
 #ifndef DC_C3C_MINW
 #define DC_C3C_MINW 4
@@ -1653,11 +1714,11 @@ hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
                           const Range* rng_ch, const u32* mw, PerftResult* res) {
   if (stm_g) {
-    auto k = k_count3c<1, 256 * DC_C3C_SLOTS, DC_C3C_MINW>;
+    auto k = k_count3c<1, kC3cCap, DC_C3C_MINW>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
                        res->divide, &res->next_chunk);
   } else {
-    auto k = k_count3c<0, 256 * DC_C3C_SLOTS, DC_C3C_MINW>;
+    auto k = k_count3c<0, kC3cCap, DC_C3C_MINW>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
                        res->divide, &res->next_chunk);
   }

@@ -23,6 +23,8 @@ flags_of() {
     soa_pad3) echo "-DDC_C2C_SOA=1 -DDC_SHIFT_PAD=3" ;;   # plain C shifts
     soa_log) echo "-DDC_C2C_SOA=1 -DDC_C3C_LOG=1" ;;      # + per-group histogram log (dc_ab_c3c_log)
     aos_log) echo "-DDC_C3C_LOG=1" ;;
+    rec) echo "-DDC_C2C_REC=1" ;;                          # 48-byte parent records (one LDS address per thread)
+    soa_otid) echo "-DDC_C2C_SOA=1" ;;                     # the soa layout built from the spill-free (otid) source
     *) echo "unknown variant $1" >&2; exit 1 ;;
   esac
 }
