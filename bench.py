@@ -128,11 +128,11 @@ class Dist:
         return float(t.item())
 
 
-def perft_step(eng, d, args, pos, depth):
-    """One perft: this rank's contiguous shard of the ply-`split` frontier on its
+def perft_step(eng, d, args, pos, depth, rules=dchess.RULES_REF):
+    """One perft: this rank's strided shard of the ply-`split` frontier on its
     GPU, then the per-root-move all-reduce (RCCL) -- dchess/dist.py."""
-    return sharded_perft(lambda p, depth, split, r, w: eng.perft_shard(p, depth, split, r, w), pos, depth,
-                         args.split, d.rank, d.world, reduce=d.allreduce_u64)
+    return sharded_perft(lambda p, depth, split, r, w: eng.perft_shard(p, depth, split, r, w, rules=rules), pos,
+                         depth, args.split, d.rank, d.world, reduce=d.allreduce_u64)
 
 
 def host_cores():
@@ -203,7 +203,7 @@ def cpu_baselines(args, threads, replay_host=None):
     return out
 
 
-def timed_perft(eng, d, args, pos, depth, steps, warmup):
+def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF, want=None):
     """warmup + exactly `steps` timed perft(depth) steps (barrier + device sync on
     both sides, max over ranks), parity-checked against the golden count.
 
@@ -214,23 +214,24 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup):
     runs over RCCL on the device, bucketed into one collective after the last
     step (K x 258 x 8 B instead of K tiny ones); the reduced totals are checked
     after the timed region."""
-    want = REF_STARTPOS.get(depth)
+    if want is None and rules == dchess.RULES_REF:
+        want = REF_STARTPOS.get(depth)
     for _ in range(warmup):  # host path: also captures the launch graph for this shard
-        tot, _, _ = perft_step(eng, d, args, pos, depth)
+        tot, _, _ = perft_step(eng, d, args, pos, depth, rules)
         if want is not None and tot != want:
             raise SystemExit(f"parity failure: perft({depth}) = {tot}, expected {want}")
     W = 258  # divide[256], n_root | overflow << 32, total
     # the first dc_perft_repeat_device call of a configuration runs one plain
     # perft and captures the launch graph: do it here, outside the timed region
     warm = eng.alloc(W * 8)
-    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, 1, warm)
+    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, 1, warm, rules=rules)
     eng.synchronize()
     warm.free()
     if d.dist is None:
         buf = eng.alloc(steps * W * 8)
         d.sync()
         t0 = time.perf_counter()
-        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, buf)
+        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, buf, rules=rules)
         eng.synchronize()
         d.sync()
         dt = time.perf_counter() - t0
@@ -242,7 +243,7 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup):
         t = torch.zeros((steps, W), dtype=torch.int64, device=f"cuda:{d.device}")
         d.sync()
         t0 = time.perf_counter()
-        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, t.data_ptr())
+        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, t.data_ptr(), rules=rules)
         eng.synchronize()
         # the exchange step of every timed perft, bucketed: one RCCL all-reduce
         # (over xGMI) of all steps' per-root-move vectors, n_root words and totals
@@ -612,7 +613,49 @@ def cpu_txsig(threads):
                       "core; the reference's libsecp256k1 could not be built here"}
 
 
-LEGS = ("perft", "perft6", "perft8", "replay", "hash", "tx", "latency")
+LEGS = ("perft", "perft6", "perft8", "fide7", "fidesuite", "replay", "hash", "tx", "latency")
+# Published FIDE perft counts (chessprogramming wiki; tests/golden/oracle_golden.json perft_fide),
+# the C2/C3/C5 configurations under standard rules, which the reference cannot compute.
+_OG = json.load(open(os.path.join(REPO, "tests", "golden", "oracle_golden.json")))["perft_fide"]
+FIDE_SUITE = ("startpos", "kiwipete", "pos3", "pos4", "pos5", "pos6")
+
+
+def fide_leg(eng, d, args, name, depth, keys, pmc_key):
+    """FIDE perft (DC_RULES_FIDE: castling, en passant, promotion, no self-check)
+    of one or more positions, each timed like the headline (dc_perft_repeat_device
+    steps, parity against the published table) and summed: value = all leaves /
+    all timed wall time.  The final stage is k_count2b (FIDE: the last ply bulk
+    counted per child with pin/check masks; DESIGN.md section 3.2 says why the
+    REF two-ply split cannot apply)."""
+    steps = max(2, args.steps // 4)
+    leaves, dt, per = 0, 0.0, {}
+    kms, kunits, kl = 0.0, 0, 0
+    for k in keys:
+        pos = dchess.pos_from_fen(_OG[k]["fen"])
+        want = _OG[k]["perft"][str(depth)]
+        lv, t = timed_perft(eng, d, args, pos, depth, steps, 1, rules=dchess.RULES_FIDE, want=want)
+        leaves += lv
+        dt += t
+        per[k] = {"leaves": want, "ms_per_step": 1e3 * t / steps}
+        eng.reset_stats()
+        eng.set_profiling(True)
+        perft_step(eng, d, args, pos, depth, dchess.RULES_FIDE)
+        d.sync()
+        eng.set_profiling(False)
+        ks = eng.kernel_stats("count2")
+        kms += ks["total_ms"]
+        kl += ks["launches"]
+        kunits += want // d.world
+    out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
+           "workload": name, "rules": "FIDE", "scaling": "strong", "leaves_per_step": leaves // steps,
+           "parity": "published tables (chessprogramming wiki), every timed step", "positions": per,
+           "final_kernel_ms": kms}
+    rec = _pmc(pmc_key) if d.world == 1 else None
+    if rec and kl and kms > 0:
+        out["roofline"] = valu_roof("k_count2b", kunits / (kms / 1e3), "leaf", W_COUNT2, rec,
+                                    "valu_lane_ops_per_leaf")
+        out["roofline"]["kernel_leaves_per_s"] = kunits / (kms / 1e3)
+    return out
 
 
 def perft8_leg(eng, d, args, pos):
@@ -663,7 +706,7 @@ def main():
         if args.no_perft:
             legs -= {"perft"}
         if args.profile_only:  # rocprof passes: headline (or replay + tx with --no-perft) only
-            legs -= {"perft6", "perft8", "hash", "latency"}
+            legs -= {"perft6", "perft8", "fide7", "fidesuite", "hash", "latency"}
             if not args.no_perft:
                 legs -= {"tx"}
         if args.no_replay or args.games <= 0:
@@ -688,6 +731,12 @@ def main():
               "scaling": "strong"}
     if "perft8" in legs:
         p8 = perft8_leg(eng, d, args, pos)
+    f7 = fs = None
+    if "fide7" in legs:  # BASELINE configs[4]'s perft(startpos, 7) under standard rules
+        f7 = fide_leg(eng, d, args, "perft(startpos, 7) RULES_FIDE", 7, ("startpos",), "fide_d7")
+    if "fidesuite" in legs:  # BASELINE configs[2]: Kiwipete + the standard suite at depth 5
+        fs = fide_leg(eng, d, args, "Kiwipete + perft suite positions 3-6 + startpos at depth 5, RULES_FIDE", 5,
+                      FIDE_SUITE, "fide_suite_d5")
 
     # --------------------------------------------------------------- replay
     replay = None
@@ -727,6 +776,10 @@ def main():
         line["perft8"] = p8
     if p6 is not None:
         line["perft6"] = p6
+    if f7 is not None:
+        line["fide_perft7"] = f7
+    if fs is not None:
+        line["fide_suite_d5"] = fs
     if shash is not None:
         line["state_hash"] = shash
     if replay is not None:

@@ -682,6 +682,7 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
   }
 }
 
+#ifdef DC_AB_KNOBS  // round-1 generator, kept for A/B measurement only (DC_GEN=1)
 __global__ __launch_bounds__(256) void k_gen_games_ref_v1(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
                                                           u32 noise_per_256, uint16_t* __restrict__ out) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
@@ -714,6 +715,7 @@ __global__ __launch_bounds__(256) void k_gen_games_ref_v1(u64 seed, u64 first_ga
     }
   }
 }
+#endif  // DC_AB_KNOBS
 
 // ------------------------------------------------------------- FIDE (K1/K2/K5)
 __global__ __launch_bounds__(256) void k_validate_fide(const DevPos* __restrict__ pos, const uint16_t* __restrict__ moves,
@@ -944,13 +946,18 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
 hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
                                 uint16_t* out) {
   if (n_games == 0) return hipSuccess;
+#ifdef DC_AB_KNOBS
   // DC_GEN=1 (A/B build only): the round-1 per-piece generator
   static const bool v1 = [] {
     const char* e = ab_env("DC_GEN");
     return e && e[0] == '1';
   }();
-  hipLaunchKernelGGL(v1 ? k_gen_games_ref_v1 : k_gen_games_ref, dim3(blocks_for(n_games, 256)), dim3(256), 0, st, seed,
-                     first_game, n_games, n_plies, noise, out);
+  auto kg = v1 ? k_gen_games_ref_v1 : k_gen_games_ref;
+#else
+  auto kg = k_gen_games_ref;
+#endif
+  hipLaunchKernelGGL(kg, dim3(blocks_for(n_games, 256)), dim3(256), 0, st, seed, first_game, n_games, n_plies, noise,
+                     out);
   return hipGetLastError();
 }
 

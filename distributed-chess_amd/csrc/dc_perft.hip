@@ -753,6 +753,7 @@ struct C2Shared {
   u64 hist[256];
 };
 
+#ifdef DC_AB_KNOBS  // round-1 final stage, kept for A/B measurement only
 template <class R, int STM>
 __global__ __launch_bounds__(256, 4) void k_count2(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                 const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
@@ -818,6 +819,7 @@ __global__ __launch_bounds__(256, 4) void k_count2(const Board* __restrict__ nod
   }
   tag_hist_flush(sh.hist, divide);
 }
+#endif  // DC_AB_KNOBS
 
 // ---------------------------------------------------- k_count2b (final stage)
 // The last two plies, one block = 256 parents (one per lane).  Their children
@@ -1582,6 +1584,7 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
   return hipGetLastError();
 }
 
+#ifdef DC_AB_KNOBS
 // Final-stage selection (for A/B measurement): DC_FINAL=2b forces k_count2b
 // under REF (k_count2c: 24 child slots per parent, the best of 20/24/28).
 static int final_variant() {
@@ -1591,6 +1594,7 @@ static int final_variant() {
   }();
   return v;
 }
+#endif
 
 template <u32 CAP, int PHASE, bool BULK, int MINW = 4>
 static void launch_count2c_cap(hipStream_t st, int stm, const Board* nodes, const uint16_t* tags, const Range* rng,
@@ -1725,12 +1729,28 @@ hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const u
   return hipGetLastError();
 }
 
+// Product: REF -> k_count2c (the bulk split), FIDE -> k_count2b<FideRules>.
+// k_count2 and k_count2b<RefRules> are compiled only into the A/B build.
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
                         const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res) {
-  if (plies == 1) DC_LAUNCH_RULES_STM(k_count1, grid_for(n_bound, 256), 256, st, nodes, meta, tags, rng, divide);
-  else if (res == nullptr && rules == 0 && final_variant() != 0) launch_count2c(st, stm, nodes, tags, rng, divide);
-  else if (res == nullptr) DC_LAUNCH_RULES_STM(k_count2b, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
-  else DC_LAUNCH_RULES_STM(k_count2, grid_for(n_bound, 64 * kC2Waves), 256, st, nodes, meta, tags, rng, divide, res);
+  if (plies == 1) {
+    DC_LAUNCH_RULES_STM(k_count1, grid_for(n_bound, 256), 256, st, nodes, meta, tags, rng, divide);
+    return hipGetLastError();
+  }
+#ifdef DC_AB_KNOBS
+  if (res != nullptr) {
+    DC_LAUNCH_RULES_STM(k_count2, grid_for(n_bound, 64 * kC2Waves), 256, st, nodes, meta, tags, rng, divide, res);
+    return hipGetLastError();
+  }
+  if (rules == 0 && final_variant() == 0) {
+    DC_LAUNCH_STM(k_count2b, RefRules, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
+    return hipGetLastError();
+  }
+#else
+  (void)res;
+#endif
+  if (rules == 0) launch_count2c(st, stm, nodes, tags, rng, divide);
+  else DC_LAUNCH_STM(k_count2b, FideRules, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
   return hipGetLastError();
 }
 

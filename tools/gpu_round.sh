@@ -49,6 +49,31 @@ if has pmc; then
     --units "replay=k_replay_ref4=799999953" --units "gen_games=k_gen_games_ref=799999953" \
     --units "state_hash=k_state_hash_ref=1000000" --units "verify_tx=k_verify_tx=262144" > $O/pmc_summary.txt
 fi
+if has fidepmc; then
+  # FIDE final stage (k_count2b<FideRules>): one bench process per leg so each
+  # key's per-dispatch average comes from one workload; merged into pmc_latest.json
+  rm -rf $O/pmc_f*
+  for leg in fide7 fidesuite; do
+    P="--steps 8 --warmup 1 --no-cpu --only $leg"
+    fpass() { local c=$1 t=$2; step "pmc $t"; timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err; }
+    fpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" f1$leg && \
+    fpass "FETCH_SIZE" f2$leg && fpass "WRITE_SIZE" f3$leg && \
+    fpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" f4$leg || { tail $O/pmc.err; exit 8; }
+    mkdir -p $O/$leg && mv $O/pmc_f[1-4]$leg $O/$leg/
+  done
+  python tools/pmc_summary.py $O/fide7 --json $O/pmc_fide7.json --source "rocprofv3 --pmc (4 passes), bench.py --only fide7" \
+    --units "fide_d7=k_count2b<dc::FideRules=3195901860" > $O/pmc_fide.txt
+  python tools/pmc_summary.py $O/fidesuite --json $O/pmc_fidesuite.json --source "rocprofv3 --pmc (4 passes), bench.py --only fidesuite" \
+    --units "fide_suite_d5=k_count2b<dc::FideRules=78180160" >> $O/pmc_fide.txt
+  python - <<'PY'
+import json, os
+p = "gpurun_out/pmc_latest.json"
+a = json.load(open(p)) if os.path.exists(p) else json.load(open("profiles/pmc_latest.json"))
+for f in ("gpurun_out/pmc_fide7.json", "gpurun_out/pmc_fidesuite.json"):
+    a.update(json.load(open(f)))
+json.dump(a, open(p, "w"), indent=1)
+PY
+fi
 if has txpmc; then
   rm -rf $O/pmc_t*
   P="--steps 1 --warmup 0 --no-cpu --profile-only --no-perft --no-replay --tx-steps 1"
