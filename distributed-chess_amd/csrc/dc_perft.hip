@@ -81,7 +81,18 @@ __device__ __forceinline__ u32 count_rt(const Board& b, u32 meta, u32 stm) {
 // wave's index (an SGPR): an opaque statement the compiler cannot hoist or
 // merge, so no thread-index-derived address stays live (and spills) across
 // the final stage's register-heavy code (round 3: k_count3c spill-free).
+// DC_C2C_LIVE_TID=1 (A/B only) restores the round-2 code generation: the
+// plain thread index, kept live by the compiler and spilled at 4 waves/SIMD
+// (with -DDC_C2C_REC=0 -DDC_C2C_SOA=1: a layout of the round-2 failing kind;
+// tools/c2c_variants.sh soa_r2 rebuilds the exact failing source).
+#ifndef DC_C2C_LIVE_TID
+#define DC_C2C_LIVE_TID 0
+#endif
 __device__ __forceinline__ u32 otid(u32 wave) {
+#if DC_C2C_LIVE_TID
+  (void)wave;
+  return threadIdx.x;
+#endif
   u32 t;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0\n\tv_lshl_add_u32 %0, %1, 6, %0"
                : "=&v"(t)
@@ -943,10 +954,12 @@ struct C2cParents {
 };
 
 #ifndef DC_C2C_REC
-#define DC_C2C_REC 0
+#define DC_C2C_REC 1
 #endif
-// DC_C2C_REC = 1: each parent's board, rays, base count and tag in one 48-byte
-// record (one per-thread LDS address instead of four differently scaled ones).
+// DC_C2C_REC = 1 (shipped since round 3): each parent's board, rays, base
+// count and tag in one 48-byte record -- one per-thread LDS address instead of
+// four differently scaled ones, and one record read per candidate child
+// (perft(7) final stage 0.482 -> 0.477 ms, same-box).  0: the round-2 arrays.
 struct alignas(16) C2cRec {
   u64 b0, b1, b2, b3, att;
   u32 base;
@@ -1198,7 +1211,8 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
   [[maybe_unused]] u64 t_entry = 0, t_wait = 0, t_last = 0, n_chunks = 0;
   if constexpr (PHASE == 8) t_entry = wall_clock64();
   tag_hist_init(sh.hist);
-  const u32 tid = threadIdx.x;
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const bool t0 = wave == 0 && lane_id() == 0;
   const u64 lo = rng->lo, hi = rng->hi;
   // Blocks take 256-parent chunks from a counter: the cost of a chunk varies
   // with its positions, and static ranges left the slowest block behind (a
@@ -1207,7 +1221,7 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
   for (;;) {
     [[maybe_unused]] u64 ta = 0;
     if constexpr (PHASE == 8) ta = wall_clock64();
-    if (tid == 0) sh.next = atomicAdd(next_chunk, 1u);
+    if (t0) sh.next = atomicAdd(next_chunk, 1u);
     __syncthreads();
     if constexpr (PHASE == 8) {
       t_last = wall_clock64();
@@ -1216,7 +1230,7 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
     const u64 s = lo + (u64)sh.next * kChunk;
     if (s >= hi) break;  // block-uniform
     if constexpr (PHASE == 8) ++n_chunks;
-    const u64 i = s + tid;
+    const u64 i = s + otid(wave);
     const bool valid = i < hi;
     Board p{0, 0, 0, 0};
     u32 tag = 0;
@@ -1224,12 +1238,12 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
       p = load_board(nodes, i);
       tag = tags[i];
     }
-    c2c_group<STM, CAP, GP, BULK>(sh, valid, p, tag, divide, __builtin_amdgcn_readfirstlane(tid >> 6));
+    c2c_group<STM, CAP, GP, BULK>(sh, valid, p, tag, divide, wave);
   }
-  tag_hist_flush(sh.hist, divide);
+  tag_hist_flush(sh.hist, divide, otid(wave));
 #ifdef DC_AB_KNOBS
   if constexpr (PHASE == 8) {
-    if (tid == 0 && blockIdx.x < kTraceBlocks) {
+    if (t0 && blockIdx.x < kTraceBlocks) {
       u32 xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
       u64* r = g_c2c_trace + blockIdx.x * kTraceWords;

@@ -24,15 +24,25 @@ flags_of() {
     soa_log) echo "-DDC_C2C_SOA=1 -DDC_C3C_LOG=1" ;;      # + per-group histogram log (dc_ab_c3c_log)
     aos_log) echo "-DDC_C3C_LOG=1" ;;
     rec) echo "-DDC_C2C_REC=1" ;;                          # 48-byte parent records (one LDS address per thread)
-    soa_otid) echo "-DDC_C2C_SOA=1" ;;                     # the soa layout built from the spill-free (otid) source
+    soa_otid) echo "-DDC_C2C_REC=0 -DDC_C2C_SOA=1" ;;      # the soa layout built from the spill-free (otid) source
+    soa_r2) echo "-DDC_C2C_SOA=1" ;;                       # round 2's failing build, rebuilt from commit 3d8df08
     *) echo "unknown variant $1" >&2; exit 1 ;;
   esac
 }
 for v in $VARIANTS; do
   F="$(flags_of $v) $EXTRA"
   mkdir -p build/var/$v
+  SRC=csrc/dc_perft.hip
+  if [ $v = soa_r2 ]; then
+    # round 2's failing final stage exactly: dc_perft.hip and its headers as of
+    # commit 3d8df08 (thread index live across c2c_group, 44-52 B/lane of
+    # spills) with the struct-of-arrays parents
+    rm -rf build/var/soa_r2/src && mkdir -p build/var/soa_r2/src
+    git -C .. archive 3d8df08 distributed-chess_amd/csrc include | tar -x -C build/var/soa_r2/src
+    SRC=build/var/soa_r2/src/distributed-chess_amd/csrc/dc_perft.hip
+  fi
   # only dc_perft.hip depends on these flags; the rest are shared objects of the product build
-  /opt/rocm/bin/hipcc $HIPFLAGS $F -c csrc/dc_perft.hip -o build/var/$v/dc_perft.o &
+  /opt/rocm/bin/hipcc $HIPFLAGS $F -c $SRC -o build/var/$v/dc_perft.o &
 done
 wait
 for v in $VARIANTS; do
