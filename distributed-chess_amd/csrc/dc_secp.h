@@ -500,6 +500,7 @@ SECP_HD void sc_inv(Sc& r, const Sc& a) {
     sqr_wide(t, a.v);
     sc_reduce(a2, t);
   }
+#pragma unroll
   for (int i = 1; i < 8; ++i) sc_mul(tbl[i], tbl[i - 1], a2);
   Sc x = tbl[7];
   for (int k = 0; k < kWin; ++k) {
@@ -508,7 +509,13 @@ SECP_HD void sc_inv(Sc& r, const Sc& a) {
       sqr_wide(t, x.v);
       sc_reduce(x, t);
     }
-    sc_mul(x, x, tbl[kInvSched[2 * k + 1]]);
+    // the odd power by select over the 8 entries, not by a runtime index:
+    // an indexed Sc[8] lives in scratch (round 2: part of 992 B/lane)
+    const int j = kInvSched[2 * k + 1];
+    Sc m = tbl[0];
+#pragma unroll
+    for (int i = 1; i < 8; ++i) sel8(m.v, j == i, tbl[i].v, m.v);
+    sc_mul(x, x, m);
   }
   r = x;
 }
@@ -791,10 +798,12 @@ constexpr int kGTabEntries = kGTabRows * 256;
 constexpr int kQWindow = DC_SECP_QW;
 
 // bits [pos, pos + len) of the 128-bit magnitude m (zero beyond bit 127)
+// (limbs picked by select: a runtime index would put m in scratch)
+SECP_HD u32 pick4(const u32 (&m)[4], int i) { return i == 0 ? m[0] : i == 1 ? m[1] : i == 2 ? m[2] : i == 3 ? m[3] : 0u; }
 SECP_HD u32 bits128(const u32 (&m)[4], int pos, int len) {
   const int i = pos >> 5, s = pos & 31;
-  u32 v = i < 4 ? m[i] >> s : 0u;
-  if (s + len > 32 && i + 1 < 4) v |= m[i + 1] << (32 - s);
+  u32 v = pick4(m, i) >> s;
+  if (s + len > 32) v |= pick4(m, i + 1) << (32 - s);
   return v & ((1u << len) - 1u);
 }
 
@@ -888,6 +897,7 @@ SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge*
       }
     }
   }
+#pragma unroll
   for (int i = 0; i < kGTabRows; ++i) {
     const u32 b = (u1.v[i >> 2] >> (8 * (i & 3))) & 255u;
     if (b) {

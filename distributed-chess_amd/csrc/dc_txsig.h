@@ -47,7 +47,19 @@ SECP_HD void sha256_init(u32 (&h)[8]) {
   h[7] = 0x5be0cd19u;
 }
 
-SECP_HD void sha256_compress(u32 (&h)[8], const uint8_t* blk) {
+// Byte k of one lane's 64-byte SHA-256 block: byte k & 3 of the block's dword
+// k >> 2, dwords `stride` bytes apart.  Host: one contiguous block (stride 4).
+// Device: the block's 16 dwords are rows of a [16][threads] LDS array, so the
+// 64 lanes of a wave touching the same byte position hit 64 different banks
+// (a contiguous 64-byte block per lane put lanes l, l + 4, ... on one bank:
+// ~15 conflict cycles per LDS cycle, round 2).
+struct BlkRef {
+  uint8_t* p;
+  u32 stride;
+  SECP_HD uint8_t& operator[](u32 k) const { return p[(k >> 2) * stride + (k & 3)]; }
+};
+
+SECP_HD void sha256_compress(u32 (&h)[8], const BlkRef& blk) {
   constexpr u32 K[64] = {
       0x428a2f98u, 0x71374491u, 0xb5c0fbcfu, 0xe9b5dba5u, 0x3956c25bu, 0x59f111f1u, 0x923f82a4u, 0xab1c5ed5u,
       0xd807aa98u, 0x12835b01u, 0x243185beu, 0x550c7dc3u, 0x72be5d74u, 0x80deb1feu, 0x9bdc06a7u, 0xc19bf174u,
@@ -136,9 +148,10 @@ struct MsgStream {
     for (;;) {
       if (stage >= 13) return -1;
       if (stage == 1 || stage == 3) {  // a player name, JSON-escaped (serde_json ESCAPE)
-        const u32 k = stage >> 1;
-        if (pos < len[k]) {
-          const u32 c = (uint8_t)str[k][pos++];
+        const bool second = stage == 3;  // selects, not a runtime index: no scratch array
+        const u32 ln = second ? len[1] : len[0];
+        if (pos < ln) {
+          const u32 c = (uint8_t)(second ? str[1] : str[0])[pos++];
           if (c == '"' || c == '\\') {
             pend = c;
             npend = 1;
@@ -160,7 +173,7 @@ struct MsgStream {
           return (int)c;
         }
       } else if (stage == 5 || stage == 7 || stage == 9 || stage == 11) {  // a coordinate
-        const u32 v = num[(stage - 5) >> 1];
+        const u32 v = stage == 5 ? num[0] : stage == 7 ? num[1] : stage == 9 ? num[2] : num[3];
         const u32 nd = ndigits(v);
         if (pos < nd) {
           u32 q = v;
@@ -179,9 +192,9 @@ struct MsgStream {
   }
 };
 
-// SHA-256 of the message.  blk: 64 bytes of scratch (LDS on the device).
+// SHA-256 of the message.  blk: the lane's 64-byte block (LDS on the device).
 SECP_HD void message_hash(u32 (&h)[8], const char* white, u32 wl, const char* black, u32 bl, const u32 (&act)[4],
-                          uint8_t* blk) {
+                          const BlkRef& blk) {
   MsgStream ms;
   ms.str[0] = white;
   ms.str[1] = black;
@@ -281,7 +294,7 @@ SECP_HD bool str_eq(const char* a, u32 al, const char* b, u32 bl) {
 
 // One transaction: the SIG_* verdict.  turn < 0 skips the owner check.
 SECP_HD u32 check_tx(const char* white, u32 wl, const char* black, u32 bl, const u32 (&act)[4], const char* sig,
-                     u32 sl, const char* pk, u32 pl, int turn, const Ge* gtab, uint8_t* blk) {
+                     u32 sl, const char* pk, u32 pl, int turn, const Ge* gtab, const BlkRef& blk) {
   u32 h[8];
   message_hash(h, white, wl, black, bl, act, blk);
   if (!hex_ok(sig, sl)) return SIG_BAD_SIG_HEX;

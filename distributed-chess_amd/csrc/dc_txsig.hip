@@ -41,7 +41,7 @@ __global__ __launch_bounds__(kTxThreads, DC_TX_MINW) void k_verify_tx(const char
                                                           const int8_t* __restrict__ turns, u32 n,
                                                           const secp::Ge* __restrict__ gtab,
                                                           uint8_t* __restrict__ verdicts) {
-  __shared__ __attribute__((aligned(16))) uint8_t blk[kTxThreads][64];  // SHA-256 block per lane
+  __shared__ __attribute__((aligned(16))) uint8_t blk[16][kTxThreads][4];  // SHA-256 blocks, dword-major (BlkRef)
   const u32 i = blockIdx.x * kTxThreads + threadIdx.x;
   if (i >= n) return;
   const size_t b = (size_t)4 * i;
@@ -49,7 +49,8 @@ __global__ __launch_bounds__(kTxThreads, DC_TX_MINW) void k_verify_tx(const char
   const u32 act[4] = {actions[b], actions[b + 1], actions[b + 2], actions[b + 3]};
   const int turn = turns ? (int)turns[i] : -1;
   verdicts[i] = (uint8_t)secp::check_tx(strings + o0, o1 - o0, strings + o1, o2 - o1, act, strings + o2, o3 - o2,
-                                        strings + o3, o4 - o3, turn, gtab, blk[threadIdx.x]);
+                                        strings + o3, o4 - o3, turn, gtab,
+                                        secp::BlkRef{&blk[0][threadIdx.x][0], kTxThreads * 4});
 }
 
 hipError_t launch_secp_gtab(hipStream_t st, secp::Ge* gtab) {

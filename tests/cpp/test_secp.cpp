@@ -120,7 +120,7 @@ int main() {
       uint8_t blk[64];
       if (op == "hash") {
         u32 h[8];
-        message_hash(h, w.data(), (u32)w.size(), b.data(), (u32)b.size(), act, blk);
+        message_hash(h, w.data(), (u32)w.size(), b.data(), (u32)b.size(), act, BlkRef{blk, 4});
         for (int i = 0; i < 8; ++i) printf("%08x", h[i]);
         printf("\n");
         fflush(stdout);
@@ -130,7 +130,7 @@ int main() {
       sig = unhex(sig);
       pk = unhex(pk);
       const u32 v = check_tx(w.data(), (u32)w.size(), b.data(), (u32)b.size(), act, sig.data(), (u32)sig.size(),
-                             pk.data(), (u32)pk.size(), turn, gtab().data(), blk);
+                             pk.data(), (u32)pk.size(), turn, gtab().data(), BlkRef{blk, 4});
       std::cout << v << "\n";
     } else {
       std::cout << "?\n";

@@ -1,0 +1,55 @@
+"""The shipped REF kernels use no scratch (CPU test, reads the built library's
+gfx950 code objects).  Round 2's only wrong perft counts came from final-stage
+builds that spilled registers to scratch at 4 waves/SIMD (DESIGN.md section
+7); since round 3 every REF perft, replay and validation kernel is built
+spill-free, and this test keeps it so: .private_segment_fixed_size == 0 in the
+AMDGPU metadata of every such kernel."""
+import os
+import re
+import shutil
+import subprocess
+import tempfile
+
+import pytest
+
+import dchess
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+# mangled-name fragments of the kernels that must stay spill-free
+MUST = ("k_count3c", "k_count2c", "k_perft_dfs", "k_replay_ref4", "k_validate_ref", "k_apply_ref",
+        "k_gen_games_ref", "RefRules")
+
+
+def kernel_scratch():
+    tmp = tempfile.mkdtemp()
+    try:
+        lib = os.path.join(tmp, "lib.so")
+        shutil.copy(dchess.LIB_PATH, lib)
+        subprocess.run([os.path.join(LLVM, "llvm-objdump"), "--offloading", lib], cwd=tmp, check=True,
+                       capture_output=True)
+        out = {}
+        for f in os.listdir(tmp):
+            if not f.endswith("gfx950"):
+                continue
+            notes = subprocess.run([os.path.join(LLVM, "llvm-readelf"), "--notes", os.path.join(tmp, f)],
+                                   check=True, capture_output=True, text=True).stdout
+            name = None
+            for line in notes.splitlines():
+                m = re.match(r"\s*\.name:\s+(\S+)", line)
+                if m:
+                    name = m.group(1)
+                m = re.match(r"\s*\.private_segment_fixed_size:\s+(\d+)", line)
+                if m and name:
+                    out[name] = int(m.group(1))
+        return out
+    finally:
+        shutil.rmtree(tmp)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(LLVM, "llvm-readelf")), reason="no ROCm llvm tools")
+def test_ref_kernels_are_spill_free():
+    ks = kernel_scratch()
+    checked = {n: s for n, s in ks.items() if any(p in n for p in MUST)}
+    assert len(checked) >= 20, sorted(ks)
+    spilling = {n: s for n, s in checked.items() if s != 0}
+    assert not spilling, spilling
