@@ -1611,6 +1611,25 @@ int dc_replay_shard_range(uint64_t n_games, uint32_t shard, uint32_t n_shards, u
 // replays (dc_replay_device) shard i of the game ids; the per-shard bitmaps
 // go to device 0 with one ncclGather over xGMI (rccl.h:745) and from there to
 // the host; the five counters are folded on the host (sums mod 2^64, xor).
+// The gather layout of the replay shards (dc_replay_shard_range's contract):
+// shard i's bitmap, padded to `per` words per ply row, is block i of
+// `gathered` ([n_shards][n_plies][per]); its first ceil(count_i / 64) words of
+// each row go to word first_i / 64 of the whole batch's row.
+int dc_replay_scatter_shards(uint64_t n_games, uint32_t n_shards, uint32_t n_plies, const uint64_t* gathered,
+                             uint64_t* bitmap) {
+  if (n_shards == 0 || (n_games && n_plies && (!gathered || !bitmap))) return DC_EINVAL;
+  const u64 words = (n_games + 63) / 64, per = (words + n_shards - 1) / n_shards;
+  for (u32 i = 0; i < n_shards; ++i) {
+    uint64_t first = 0, cnt = 0;
+    const int r = dc_replay_shard_range(n_games, i, n_shards, &first, &cnt);
+    if (r != DC_SUCCESS) return r;
+    const u64 w_r = (cnt + 63) / 64;
+    for (u32 p = 0; p < n_plies && w_r; ++p)
+      std::memcpy(bitmap + (size_t)p * words + first / 64, gathered + ((size_t)i * n_plies + p) * per, w_r * 8);
+  }
+  return DC_SUCCESS;
+}
+
 int dc_multi_replay(const int* devices, int n_devices, uint32_t rules, uint64_t seed, uint64_t n_games,
                     uint32_t n_plies, uint32_t noise_per_256, uint64_t* bitmap, dc_replay_stats* stats) {
   if (!devices || n_devices <= 0 || rules > DC_RULES_FIDE || noise_per_256 > 256) return DC_EINVAL;
@@ -1686,16 +1705,13 @@ int dc_multi_replay(const int* devices, int n_devices, uint32_t rules, uint64_t 
       }
       for (auto& cm : comms) ncclCommDestroy(cm);
     }
-    // device 0 -> host: shard i's rows land at word offset first_i / 64 of each ply row
-    for (int i = 0; i < n_devices && result == DC_SUCCESS; ++i) {
-      uint64_t first = 0, cnt = 0;
-      dc_replay_shard_range(n_games, (u32)i, (u32)n_devices, &first, &cnt);
-      const u64 w_r = (cnt + 63) / 64;
-      if (!w_r) continue;
+    // device 0 -> host, then each shard's rows to word offset first_i / 64 of
+    // every ply row (dc_replay_scatter_shards: the layout is host-tested)
+    if (result == DC_SUCCESS) {
+      std::vector<u64> all((size_t)n_devices * shard_words);
       (void)hipSetDevice(devices[0]);
-      if (hipMemcpy2D(bitmap + first / 64, words * 8, static_cast<const u64*>(d_all) + (size_t)i * shard_words,
-                      per * 8, w_r * 8, n_plies, hipMemcpyDeviceToHost) != hipSuccess)
-        result = DC_EHIP;
+      if (hipMemcpy(all.data(), d_all, all.size() * 8, hipMemcpyDeviceToHost) != hipSuccess) result = DC_EHIP;
+      else result = dc_replay_scatter_shards(n_games, (u32)n_devices, n_plies, reinterpret_cast<const uint64_t*>(all.data()), bitmap);
     }
   }
   if (result == DC_SUCCESS && stats) {

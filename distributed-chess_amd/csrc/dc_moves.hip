@@ -628,8 +628,9 @@ __device__ __forceinline__ u32 ref_kth_move(const Board& b, u32 stm, u32 k) {
 // (k_gen_games_ref_v1: a per-piece loop with a per-kind switch) issued 3,842
 // VALU per wave and ply with 22 % of lanes active.  Same games, bit for bit
 // (tests/golden: C4 moves SHA-256).
-__global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
-                                                       u32 noise_per_256, uint16_t* __restrict__ out) {
+#ifdef DC_AB_KNOBS  // round-2 generator, kept for A/B measurement only (DC_GEN=2)
+__global__ __launch_bounds__(256) void k_gen_games_ref_v2(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
+                                                          u32 noise_per_256, uint16_t* __restrict__ out) {
   const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= n_games) return;
   u64 s = seed ^ (first_game + g);
@@ -672,6 +673,185 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
     const u64 tv = ref_piece_targets_w(w, (int)(f ^ flip));
     const u64 treal = stm ? flip_rows(tv) : tv;
     const u32 kth = (n && k - clo < (u32)__popcll(treal)) ? (f | (select_bit_bf(treal, k - clo) << 6)) : 0u;
+    const u32 m = noise ? (u32)((r >> 8) & 0xFFF) : kth;
+    *slot = over ? (uint16_t)0xFFFF : (uint16_t)m;
+    const bool ok = !over && (!noise || ref_verdict(b, stm, m) == V_OK);
+    if (ok) {
+      ref_make(b, (int)(m & 63), (int)((m >> 6) & 63));
+      stm ^= 1;
+    }
+  }
+}
+#endif  // DC_AB_KNOBS
+
+// K5, round 3 (k_gen_games_ref).  The same games as round 2 (the k-th move in
+// (from, to) order of real squares; C4's moves SHA-256 is the check), with
+// the per-ply work restructured so that no source-restricted bulk count is
+// repeated:
+//   - pawns as four direction source sets (push, double push, two captures),
+//     whose restricted counts are four masked popcounts;
+//   - every other piece (at most 2 knights, 1 king, 3 diagonal and 3
+//     orthogonal sliders from startpos: REF never adds a piece) as a slot
+//     holding its real square and its move count, its targets from LDS tables
+//     (knight, king, and per-direction rays whose first blocker is one
+//     lsb/msb: r ^ ray[first blocker]);
+//   - the source square of the k-th move by a 6-step binary search over real
+//     squares on those slots and sets (round 2: four source-restricted bulk
+//     counts with slider fills, 1,662 VALU per move);
+//   - only the chosen piece's targets are built again.
+struct GenTabs {
+  u64 ray[8][64];  // 0 N, 1 S, 2 E, 3 W, 4 NE, 5 SW, 6 NW, 7 SE: squares beyond s to the edge
+  u64 kn[64], kg[64];
+};
+
+__device__ __forceinline__ void gen_tabs_build(GenTabs& T) {
+  constexpr int dx[8] = {1, -1, 0, 0, 1, -1, 1, -1}, dy[8] = {0, 0, 1, -1, 1, -1, -1, 1};
+  for (u32 e = threadIdx.x; e < 8 * 64; e += blockDim.x) {
+    const int d = (int)(e >> 6), sq = (int)(e & 63);
+    u64 r = 0;
+    int x = (sq >> 3) + dx[d], y = (sq & 7) + dy[d];
+    while (x >= 0 && x < 8 && y >= 0 && y < 8) {
+      r |= 1ull << (8 * x + y);
+      x += dx[d];
+      y += dy[d];
+    }
+    T.ray[d][sq] = r;
+  }
+  for (u32 sq = threadIdx.x; sq < 64; sq += blockDim.x) {
+    const int x = (int)(sq >> 3), y = (int)(sq & 7);
+    u64 kn = 0, kg = 0;
+    for (int a = -2; a <= 2; ++a)
+      for (int c = -2; c <= 2; ++c) {
+        const int X = x + a, Y = y + c;
+        if (X < 0 || X > 7 || Y < 0 || Y > 7) continue;
+        const int aa = a < 0 ? -a : a, cc = c < 0 ? -c : c;
+        if (aa * cc == 2) kn |= 1ull << (8 * X + Y);
+        if (aa <= 1 && cc <= 1 && (aa | cc)) kg |= 1ull << (8 * X + Y);
+      }
+    T.kn[sq] = kn;
+    T.kg[sq] = kg;
+  }
+}
+
+// Ray of direction D from s up to and including the first occupied square:
+// the table ray minus the ray beyond that blocker (a sentinel blocker on the
+// edge square whose ray is empty makes the unblocked case the same formula).
+template <int D>
+__device__ __forceinline__ u64 gen_ray(const GenTabs& T, int s, u64 occ) {
+  const u64 r = T.ray[D][s];
+  const u64 bl = r & occ;
+  const int b = (D & 1) == 0 ? lsb(bl | (1ull << 63)) : msb(bl | 1ull);
+  return r ^ T.ray[D][b];
+}
+
+__global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
+                                                       u32 noise_per_256, uint16_t* __restrict__ out) {
+  __shared__ GenTabs T;
+  gen_tabs_build(T);
+  __syncthreads();
+  const u32 g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= n_games) return;
+  u64 s = seed ^ (first_game + g);
+  Board b{0, 0, 0, 0};
+  startpos_board(b);
+  u32 stm = 0;
+  bool over = false;
+  for (u32 ply = 0; ply < n_plies; ++ply) {
+    uint16_t* slot = out + (size_t)ply * n_games + g;
+    const Board w = view_sel(b, stm);  // white to move (rows flipped for Black)
+    const u32 flip = stm ? 56u : 0u;
+    const Sides sw = sides<0>(w);
+    const u64 E = sw.empty, no = sw.notown, occ = sw.occ;
+    // pawn sources per direction class (ref_count_from_w's pawn terms)
+    const u64 S1 = sw.P & sh<-8>(E);
+    const u64 S2 = S1 & kRow(1) & sh<-16>(E);
+    const u64 SL = sw.P & sh<-7>(sw.enemy & kNotH);
+    const u64 SR = sw.P & sh<-9>(sw.enemy & kNotA);
+    u32 n = pc(S1) + pc(S2) + pc(SL) + pc(SR);
+    // piece slots: (real square << 8) | move count; square 64 = empty slot
+    u32 sl[9];
+    auto take = [](u64& rem, int& sv) {  // next piece of a set: its view square, or -1
+      const bool any = rem != 0;
+      sv = any ? lsb(rem) : 0;
+      rem &= rem - 1;
+      return any;
+    };
+    {
+      u64 rem = sw.N;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        int sv;
+        const bool any = take(rem, sv);
+        const u32 c = any ? pc(T.kn[sv] & no) : 0u;
+        sl[j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+        n += c;
+      }
+      rem = sw.K;
+      int sv;
+      const bool any = take(rem, sv);
+      const u32 c = any ? pc(T.kg[sv] & no) : 0u;
+      sl[2] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+      n += c;
+    }
+    {
+      u64 rem = sw.D;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        int sv;
+        const bool any = take(rem, sv);
+        const u64 t = gen_ray<4>(T, sv, occ) | gen_ray<5>(T, sv, occ) | gen_ray<6>(T, sv, occ) | gen_ray<7>(T, sv, occ);
+        const u32 c = any ? pc(t & no) : 0u;
+        sl[3 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+        n += c;
+      }
+      rem = sw.O;
+#pragma unroll
+      for (int j = 0; j < 3; ++j) {
+        int sv;
+        const bool any = take(rem, sv);
+        const u64 t = gen_ray<0>(T, sv, occ) | gen_ray<1>(T, sv, occ) | gen_ray<2>(T, sv, occ) | gen_ray<3>(T, sv, occ);
+        const u32 c = any ? pc(t & no) : 0u;
+        sl[6 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+        n += c;
+      }
+    }
+    if (over) n = 0;
+    over = n == 0;
+    u64 r = 0;
+    if (!over) r = splitmix_next(s);
+    const bool noise = (u32)(r & 0xFF) < noise_per_256;
+    const u32 k = (u32)(((r >> 32) * (u64)n) >> 32);
+    // the k-th move's real source square: the first x with D(x) > k, where
+    // D(x) = moves whose real source square is <= x
+    u32 lo = 0, dlo = 0;
+#pragma unroll
+    for (u32 step = 32; step; step >>= 1) {
+      const u32 x = lo + step - 1;
+      const u64 mr = (2ull << x) - 1;  // real squares <= x (x = 63: all)
+      const u64 mv = stm ? flip_rows(mr) : mr;
+      u32 d = pc(S1 & mv) + pc(S2 & mv) + pc(SL & mv) + pc(SR & mv);
+#pragma unroll
+      for (int j = 0; j < 9; ++j) d += (sl[j] >> 8) <= x ? (sl[j] & 0xFF) : 0u;
+      if (d <= k) {
+        lo = x + 1;
+        dlo = d;
+      }
+    }
+    const u32 f = lo;  // real
+    const int fv = (int)(f ^ flip) & 63;
+    const u64 bit = 1ull << fv;
+    // targets of the piece on fv (view), every class masked by its kind
+    u64 tv = (((S1 & bit) != 0) ? sh<8>(bit) : 0ull) | (((S2 & bit) != 0) ? sh<16>(bit) : 0ull) |
+             (((SL & bit) != 0) ? sh<7>(bit) : 0ull) | (((SR & bit) != 0) ? sh<9>(bit) : 0ull);
+    u64 tp = ((sw.N & bit) != 0 ? T.kn[fv] : 0ull) | ((sw.K & bit) != 0 ? T.kg[fv] : 0ull);
+    if ((sw.D & bit) != 0)
+      tp |= gen_ray<4>(T, fv, occ) | gen_ray<5>(T, fv, occ) | gen_ray<6>(T, fv, occ) | gen_ray<7>(T, fv, occ);
+    if ((sw.O & bit) != 0)
+      tp |= gen_ray<0>(T, fv, occ) | gen_ray<1>(T, fv, occ) | gen_ray<2>(T, fv, occ) | gen_ray<3>(T, fv, occ);
+    tv |= tp & no;
+    const u64 treal = stm ? flip_rows(tv) : tv;
+    const u32 kk = k - dlo;
+    const u32 kth = (n && kk < (u32)__popcll(treal)) ? (f | (select_bit_bf(treal, kk) << 6)) : 0u;
     const u32 m = noise ? (u32)((r >> 8) & 0xFFF) : kth;
     *slot = over ? (uint16_t)0xFFFF : (uint16_t)m;
     const bool ok = !over && (!noise || ref_verdict(b, stm, m) == V_OK);
@@ -947,12 +1127,16 @@ hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_
                                 uint16_t* out) {
   if (n_games == 0) return hipSuccess;
 #ifdef DC_AB_KNOBS
-  // DC_GEN=1 (A/B build only): the round-1 per-piece generator
+  // DC_GEN=1 / 2 (A/B build only): the round-1 / round-2 generators
   static const bool v1 = [] {
     const char* e = ab_env("DC_GEN");
     return e && e[0] == '1';
   }();
-  auto kg = v1 ? k_gen_games_ref_v1 : k_gen_games_ref;
+  static const bool v2 = [] {
+    const char* e = ab_env("DC_GEN");
+    return e && e[0] == '2';
+  }();
+  auto kg = v1 ? k_gen_games_ref_v1 : v2 ? k_gen_games_ref_v2 : k_gen_games_ref;
 #else
   auto kg = k_gen_games_ref;
 #endif

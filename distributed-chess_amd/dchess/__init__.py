@@ -104,6 +104,7 @@ def lib():
                                      C.POINTER(C.c_uint64)]),
         "dc_replay_shard_range": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint64),
                                             C.POINTER(C.c_uint64)]),
+        "dc_replay_scatter_shards": (C.c_int, [C.c_uint64, C.c_uint32, C.c_uint32, _vp, _vp]),
         "dc_multi_replay": (C.c_int, [_vp, C.c_int, C.c_uint32, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32,
                                       _vp, C.POINTER(_Stats)]),
         "dc_keccak256": (C.c_int, [_vp, C.c_size_t, _vp]),

@@ -322,6 +322,13 @@ int dc_multi_perft(const int* devices, int n_devices, uint32_t rules, const dc_p
  * replay their own range and combine: validated / accepted / rejected /
  * digest_sum add (mod 2^64), digest_xor xors, bitmaps are gathered. */
 int dc_replay_shard_range(uint64_t n_games, uint32_t shard, uint32_t n_shards, uint64_t* first, uint64_t* count);
+/* The combine of the shards' bitmaps (host memory): gathered = n_shards blocks
+ * [n_plies][per] with per = ceil(ceil(n_games/64) / n_shards) (each shard's
+ * ply-major bitmap padded to `per` words per row, as a gather collects them);
+ * bitmap = the whole batch's [n_plies][ceil(n_games/64)].  dc_multi_replay's
+ * last step, and the layout a torch.distributed caller's gather produces. */
+int dc_replay_scatter_shards(uint64_t n_games, uint32_t n_shards, uint32_t n_plies, const uint64_t* gathered,
+                             uint64_t* bitmap);
 /* The seeded games [0, n_games) (dc_gen_games' generator: seed, n_plies,
  * noise_per_256) generated and replayed on n_devices GPUs of one process,
  * shard i on device i.  bitmap (optional, HOST) = the whole batch's ply-major

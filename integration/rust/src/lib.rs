@@ -147,6 +147,8 @@ pub mod sys {
                               divide: *mut u64, root_moves: *mut u16, n_root: *mut u32, total: *mut u64) -> c_int;
         pub fn dc_replay_shard_range(n_games: u64, shard: u32, n_shards: u32, first: *mut u64,
                                      count: *mut u64) -> c_int;
+        pub fn dc_replay_scatter_shards(n_games: u64, n_shards: u32, n_plies: u32, gathered: *const u64,
+                                        bitmap: *mut u64) -> c_int;
         pub fn dc_multi_replay(devices: *const c_int, n_devices: c_int, rules: u32, seed: u64, n_games: u64,
                                n_plies: u32, noise_per_256: u32, bitmap: *mut u64,
                                stats: *mut dc_replay_stats) -> c_int;
