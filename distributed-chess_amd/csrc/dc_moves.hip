@@ -799,8 +799,11 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
       for (int j = 0; j < 3; ++j) {
         int sv;
         const bool any = take(rem, sv);
-        const u64 t = gen_ray<4>(T, sv, occ) | gen_ray<5>(T, sv, occ) | gen_ray<6>(T, sv, occ) | gen_ray<7>(T, sv, occ);
-        const u32 c = any ? pc(t & no) : 0u;
+        u32 c = 0;
+        if (any) {  // skipped by a wave none of whose games has a j-th such slider
+          const u64 t = gen_ray<4>(T, sv, occ) | gen_ray<5>(T, sv, occ) | gen_ray<6>(T, sv, occ) | gen_ray<7>(T, sv, occ);
+          c = pc(t & no);
+        }
         sl[3 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
@@ -809,8 +812,11 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
       for (int j = 0; j < 3; ++j) {
         int sv;
         const bool any = take(rem, sv);
-        const u64 t = gen_ray<0>(T, sv, occ) | gen_ray<1>(T, sv, occ) | gen_ray<2>(T, sv, occ) | gen_ray<3>(T, sv, occ);
-        const u32 c = any ? pc(t & no) : 0u;
+        u32 c = 0;
+        if (any) {
+          const u64 t = gen_ray<0>(T, sv, occ) | gen_ray<1>(T, sv, occ) | gen_ray<2>(T, sv, occ) | gen_ray<3>(T, sv, occ);
+          c = pc(t & no);
+        }
         sl[6 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
@@ -837,7 +843,12 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
         dlo = d;
       }
     }
-    const u32 f = lo;  // real
+    // the piece whose targets are needed: the k-th move's source, or a noise
+    // move's source (its verdict is then "t is one of that piece's targets":
+    // ref_verdict's REF rules, chess.rs:82-125, restated set-wise -- the same
+    // targets that give n; an empty or enemy square has none)
+    const u32 mnoise = (u32)((r >> 8) & 0xFFF);
+    const u32 f = noise ? (mnoise & 63) : lo;  // real
     const int fv = (int)(f ^ flip) & 63;
     const u64 bit = 1ull << fv;
     // targets of the piece on fv (view), every class masked by its kind
@@ -852,9 +863,9 @@ __global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game,
     const u64 treal = stm ? flip_rows(tv) : tv;
     const u32 kk = k - dlo;
     const u32 kth = (n && kk < (u32)__popcll(treal)) ? (f | (select_bit_bf(treal, kk) << 6)) : 0u;
-    const u32 m = noise ? (u32)((r >> 8) & 0xFFF) : kth;
+    const u32 m = noise ? mnoise : kth;
     *slot = over ? (uint16_t)0xFFFF : (uint16_t)m;
-    const bool ok = !over && (!noise || ref_verdict(b, stm, m) == V_OK);
+    const bool ok = !over && (!noise || ((treal >> (mnoise >> 6)) & 1) != 0);
     if (ok) {
       ref_make(b, (int)(m & 63), (int)((m >> 6) & 63));
       stm ^= 1;
