@@ -744,7 +744,10 @@ __device__ __forceinline__ u64 gen_ray(const GenTabs& T, int s, u64 occ) {
   return r ^ T.ray[D][b];
 }
 
-__global__ __launch_bounds__(256) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
+#ifndef DC_GEN_MINW
+#define DC_GEN_MINW 1
+#endif
+__global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
                                                        u32 noise_per_256, uint16_t* __restrict__ out) {
   __shared__ GenTabs T;
   gen_tabs_build(T);
