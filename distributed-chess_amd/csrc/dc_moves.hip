@@ -420,6 +420,15 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref3(Mailbox mb0, u64 occ
 // moved piece's cell kind | 8 if the target held a piece (dc_apply_batch's
 // info, what update_history needs, chess.rs:156-167), 0xFF for a rejected ply;
 // ply-major like the moves.  Compiled out of the plain replay.
+// DC_R4_LAZY = 1 (round-3 experiment, off): a vacated square is not cleared
+// in the mailbox; the occupancy bitboard masks its stale nibble when read, so
+// a make-move is one LDS read-modify-write instead of two.  Measured slower
+// (10M x 80: 0.865 -> 0.998 ms, same box, profiles/r03/ab_replay_lazy.txt):
+// the kernel is bound by its per-ply dependency chain, not by LDS cycles,
+// and the occupancy test puts a 64-bit shift on that chain.
+#ifndef DC_R4_LAZY
+#define DC_R4_LAZY 0
+#endif
 template <int LOOK, int PF, bool DW, bool INFO = false>
 __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ0, u32 stm0, const uint16_t* __restrict__ moves,
                                                            u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
@@ -496,8 +505,16 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
       const u64 bt = t0.bt;
       const u32 gw = t0.gw;
       const u32 st = (m >> 4) & 28;
+      const u32 rawt = __builtin_amdgcn_ubfe(wt, st, 4);
+#if DC_R4_LAZY
+      // a square's nibble is live only while occ has it (v_lshrrev_b64 takes
+      // the shift's low 6 bits: f = m & 63 needs no mask)
+      const u32 nib = ((u32)(occ >> (m & 63)) & 1u) ? __builtin_amdgcn_ubfe(wf, m2, 4) : 0u;
+      const u32 nibt = ((u32)(occ >> ((m >> 6) & 63)) & 1u) ? rawt : 0u;
+#else
       const u32 nib = __builtin_amdgcn_ubfe(wf, m2, 4);
-      const u32 nibt = __builtin_amdgcn_ubfe(wt, st, 4);
+      const u32 nibt = rawt;
+#endif
       const u32 x = nibt ^ stm;
       const u32 shift = nib | (__builtin_amdgcn_ubfe(kEnemyLut, x, 1) << 4);
       const u32 geo_ok = __builtin_amdgcn_ubfe(gw, shift, 1), own = __builtin_amdgcn_ubfe(kOwnLut, x, 1);
@@ -524,8 +541,10 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
         if (active) info[(size_t)p * n_games + g] = (uint8_t)(ok ? code : 0xFFu);
       }
       if (ok) {
+#if !DC_R4_LAZY
         atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + af), nib << m2);
-        atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + at), (nib ^ nibt) << st);
+#endif
+        atomicXor(reinterpret_cast<u32*>(r4_smem + kR3TabBytes + at), (nib ^ rawt) << st);
         occ = bop3<0xBA>(occ, 1ull << (m & 63), 1ull << ((m >> 6) & 63));
         stm ^= 1;
       }
@@ -568,6 +587,7 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
         b.b2 |= (u64)gather_nibble_bits(d >> 2) << (8 * j);
         b.b3 |= (u64)gather_nibble_bits(d >> 3) << (8 * j);
       }
+      if (DC_R4_LAZY) b = Board{b.b0 & occ, b.b1 & occ, b.b2 & occ, b.b3 & occ};  // stale nibbles of vacated squares
       const u64 dg = board_digest(b, stm);
       if (digests) digests[g] = dg;
       dsum += dg;

@@ -960,14 +960,36 @@ struct C2cParents {
 // count and tag in one 48-byte record -- one per-thread LDS address instead of
 // four differently scaled ones, and one record read per candidate child
 // (perft(7) final stage 0.482 -> 0.477 ms, same-box).  0: the round-2 arrays.
+// DC_C2C_DIAGQ = 1 (shipped since round 3, needs the records): full-recount
+// children whose move leaves the opponent's orthogonal group unchanged (about
+// 83 % of them at perft(7): profiles/r03/c2c_stats_d7.txt) go to a second
+// per-wave queue and are counted group-wise (ref_count_child_diag: the
+// diagonal group and the pawns recomputed, the leapers corrected at t);
+// the rest keep the full recount.
+#ifndef DC_C2C_DIAGQ
+#define DC_C2C_DIAGQ DC_C2C_REC
+#endif
+#if DC_C2C_DIAGQ && !DC_C2C_REC
+#error "DC_C2C_DIAGQ needs DC_C2C_REC"
+#endif
+#if DC_C2C_DIAGQ
+struct alignas(8) C2cRec {
+  u64 b0, b1, b2, b3, att, orth;
+  u32 base;
+  uint16_t tag, diag;
+};
+#else
 struct alignas(16) C2cRec {
   u64 b0, b1, b2, b3, att;
   u32 base;
   uint16_t tag, pad;
 };
+#endif
 // Special-child slots per group of 256 parents: 24 per parent, trimmed with
-// the 48-byte records so that four blocks' LDS (<= 40,960 B each) fit a CU.
-constexpr u32 kC2cCap = DC_C2C_REC ? 6128 : 256 * 24;
+// the 48-byte records so that four blocks' LDS (<= 40,960 B each) fit a CU;
+// 19.9 with the 56-byte records and the second queue (the mean at perft(7) is
+// 7.6: 0.306 of 24.7 children).
+constexpr u32 kC2cCap = DC_C2C_REC ? (DC_C2C_DIAGQ ? 5104 : 6128) : 256 * 24;
 
 template <u32 CAP>
 struct C2cShared {
@@ -980,14 +1002,30 @@ struct C2cShared {
 #endif
   u32 slot[CAP];
   u32 queue[4][kC2cQueue];
+#if DC_C2C_DIAGQ
+  u32 queue_d[4][kC2cQueue];
+#endif
   u64 hist[256];
   u64 wsum[4];
   u32 next;
 #if !DC_C2C_REC
   uint16_t ptag[256];
 #endif
-  __device__ __forceinline__ void put(u32 i, const Board& p, u64 a, u32 bs, u32 tg) {
-#if DC_C2C_REC
+  __device__ __forceinline__ void put(u32 i, const Board& p, u64 a, u32 bs, u32 tg, u64 orth = 0, u32 diag = 0) {
+#if DC_C2C_DIAGQ
+    (void)tg;  // written by put_tag before the parent split (fewer live VGPRs there)
+    C2cRec& r = rec[i];
+    r.b0 = p.b0;
+    r.b1 = p.b1;
+    r.b2 = p.b2;
+    r.b3 = p.b3;
+    r.att = a;
+    r.orth = orth;
+    r.base = bs;
+    r.diag = (uint16_t)diag;
+#elif DC_C2C_REC
+    (void)orth;
+    (void)diag;
     rec[i] = C2cRec{p.b0, p.b1, p.b2, p.b3, a, bs, (uint16_t)tg, 0};
 #else
     par.set(i, p);
@@ -996,11 +1034,23 @@ struct C2cShared {
     ptag[i] = (uint16_t)tg;
 #endif
   }
+  __device__ __forceinline__ void put_tag(u32 i, u32 tg) {
+#if DC_C2C_DIAGQ
+    rec[i].tag = (uint16_t)tg;
+#else
+    (void)i;
+    (void)tg;
+#endif
+  }
 #if DC_C2C_REC
   __device__ __forceinline__ Board board(u32 i) const { return Board{rec[i].b0, rec[i].b1, rec[i].b2, rec[i].b3}; }
   __device__ __forceinline__ u64 rays(u32 i) const { return rec[i].att; }
   __device__ __forceinline__ u32 basec(u32 i) const { return rec[i].base; }
   __device__ __forceinline__ u32 tag(u32 i) const { return rec[i].tag; }
+#if DC_C2C_DIAGQ
+  __device__ __forceinline__ u64 orth(u32 i) const { return rec[i].orth; }
+  __device__ __forceinline__ u32 diagc(u32 i) const { return rec[i].diag; }
+#endif
 #else
   __device__ __forceinline__ Board board(u32 i) const { return par.get(i); }
   __device__ __forceinline__ u64 rays(u32 i) const { return att[i]; }
@@ -1016,6 +1066,14 @@ __device__ __forceinline__ u32 c2c_full(const C2cShared<CAP>& sh, u32 e) {
   ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
   return ref_count<1 - STM>(ch);
 }
+
+#if DC_C2C_DIAGQ
+template <int STM, u32 CAP>
+__device__ __forceinline__ u32 c2c_diag(const C2cShared<CAP>& sh, u32 e) {
+  const u32 pl = e >> 15;
+  return ref_count_child_diag<1 - STM>(sh.board(pl), (int)(e & 63), (int)((e >> 6) & 63), sh.basec(pl) - sh.diagc(pl));
+}
+#endif
 
 // BULK: children reached by "simple" moves -- quiet, f and t off the
 // opponent's slider rays and off its pawn-sensitive squares G
@@ -1039,16 +1097,28 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   // wave: this wave's index in the block (an SGPR, readfirstlane at kernel
   // entry); the thread index is rebuilt where it is used (otid)
   const u32 w = wave, lane = lane_id();
+  // GQ: the group-wise recount queue (DC_C2C_DIAGQ) in the bulk split
+  constexpr bool GQ = DC_C2C_DIAGQ && BULK;
   u32* q = sh.queue[w];
-  u32 cnt = 0, base = 0;
-  u64 att = 0, Fs = 0, Ts = 0, simple_leaves = 0;
+#if DC_C2C_DIAGQ
+  u32* qd = sh.queue_d[w];
+#else
+  u32* qd = q;
+#endif
+  u32 cnt = 0, base = 0, diag = 0;
+  u64 att = 0, orth = 0, Fs = 0, Ts = 0, simple_leaves = 0;
   u32 nsim = 0;
+  sh.put_tag(otid(w), tag);  // (the previous group ended with a barrier)
   if (valid) {
     if constexpr (BULK) {
       ParentSplit ps;
-      ref_parent_split<STM>(p, ps);
+      ref_parent_split<STM, GQ>(p, ps);
       base = ps.base;
       att = ps.att;
+      if constexpr (GQ) {
+        orth = ps.orth;
+        diag = ps.diag;
+      }
       Fs = ps.Fs;
       Ts = ps.Ts;
       cnt = ps.n_total - ps.n_simple;  // enumerated (special) children only
@@ -1062,36 +1132,44 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   u64 total64;
   const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64, w);
   const u32 total = (u32)total64;
-  sh.put(otid(w), p, att, base, tag);
+  sh.put(otid(w), p, att, base, tag, orth, diag);
   __syncthreads();
   const u32 tag0 = sh.tag(0);
   u64 acc = 0;  // grandchildren under parents whose tag == tag0
-  auto add = [&](u32 pl, u32 k, bool live) {
+  // k leaves under the root move `ptag` (read with the record, so no LDS
+  // round trip of its own)
+  auto add_tag = [&](u32 ptag, u32 k, bool live) {
     if constexpr (PHASE == 7) return;
     if (!live) return;
-    const u32 ptag = sh.tag(pl);
     if (ptag == tag0) acc += k;
     else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
   };
-  u32 qn = 0;  // queue length: wave-uniform (kept scalar via readfirstlane)
+  auto add = [&](u32 pl, u32 k, bool live) { add_tag(sh.tag(pl), k, live); };
+  u32 qn = 0, qnd = 0;  // queue lengths: wave-uniform (kept scalar via readfirstlane)
   // One candidate child: its parent's LDS record is loaded first (so two
   // candidates' loads can be in flight together), then the short path if the
-  // move is quiet, else the child is appended to the queue.
+  // move is quiet, else the child is appended to a queue: the group-wise one
+  // (GQ) if the move is off the opponent's orthogonal group, else the full one.
   struct Cand {
-    u32 e, base;
+    u32 e, base, tag;
     Board pb;
-    u64 a;
+    u64 a, o;
   };
   auto fetch = [&](u32 e) {
     const u32 pl = e >> 15;
-    return Cand{e, sh.basec(pl), sh.board(pl), sh.rays(pl)};
+#if DC_C2C_DIAGQ
+    // the whole 56-byte record: board, rays, orthogonal group, base/tag/diag
+    return Cand{e, sh.basec(pl), sh.tag(pl), sh.board(pl), sh.rays(pl), GQ ? sh.orth(pl) : 0ull};
+#else
+    return Cand{e, sh.basec(pl), sh.tag(pl), sh.board(pl), sh.rays(pl), 0ull};
+#endif
   };
   auto consume = [&](const Cand& c, bool live) {
     const u32 pl = c.e >> 15;
     const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
     const u64 occ = occupied(c.pb);
     const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
-    if (live && quiet) add(pl, c.base + (PHASE == 6 ? (u32)t : ref_pawn_count_child<1 - STM>(c.pb, f, t)), true);
+    if (live && quiet) add_tag(c.tag, c.base + (PHASE == 6 ? (u32)t : ref_pawn_count_child<1 - STM>(c.pb, f, t)), true);
     const bool full = live && !quiet;
     const u64 em = ballot(full);
     if constexpr (PHASE == 7) {  // statistics: divide[0] quiet special children, [1] full-recount children
@@ -1121,16 +1199,44 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
         atomicAdd((unsigned long long*)(divide + 8), (unsigned long long)__popcll(m8));
       }
     }
-    if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
-    qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
+    if constexpr (GQ) {
+      const bool go = ((((c.o >> t) | (c.o >> f)) & 1) != 0);
+      const u64 ef = ballot(full && go), ed = em ^ ef;
+      const u64 below = (1ull << lane) - 1;
+      if (full) {
+        if (go) q[qn + (u32)__popcll(ef & below)] = c.e;
+        else qd[qnd + (u32)__popcll(ed & below)] = c.e;
+      }
+      qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(ef));
+      qnd = __builtin_amdgcn_readfirstlane(qnd + (u32)__popcll(ed));
+    } else {
+      if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
+      qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
+    }
   };
   auto drain64 = [&]() {  // qn >= 64: recount 64 queued children in full
     wave_lds_sync();
     const u32 e2 = q[lane];
-    add(e2 >> 15, PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2), true);
+    const u32 tg = sh.tag(e2 >> 15);  // issued with the record reads
+    add_tag(tg, PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2), true);
     wave_lds_sync();
     if (lane + 64 < qn) q[lane] = q[lane + 64];
     qn = __builtin_amdgcn_readfirstlane(qn - 64);
+  };
+  auto drain64d = [&]() {  // qnd >= 64: count 64 queued children group-wise
+#if DC_C2C_DIAGQ
+    wave_lds_sync();
+    const u32 e2 = qd[lane];
+    const u32 tg = sh.tag(e2 >> 15);
+    add_tag(tg, PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_diag<STM>(sh, e2), true);
+    wave_lds_sync();
+    if (lane + 64 < qnd) qd[lane] = qd[lane + 64];
+    qnd = __builtin_amdgcn_readfirstlane(qnd - 64);
+#endif
+  };
+  auto drain = [&]() {
+    if (qn >= 64) drain64();
+    if constexpr (GQ) if (qnd >= 64) drain64d();
   };
   if constexpr (BULK && PHASE != 7) add(otid(w), (u32)simple_leaves, valid);
   if constexpr (PHASE == 7) {  // [2] simple children, [3] parents
@@ -1144,9 +1250,22 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   for (u32 wbase = 0; wbase < (PHASE == 2 ? 0u : total); wbase += CAP) {
     if (wbase) __syncthreads();  // previous window fully read
     // each (f, t) of this parent's enumerated (BULK: special) moves -> visit(f, t)
+    // the parent is read back from its record (after the barrier: a fresh
+    // LDS read), so its board is not live across the consume/drain loop
+    // (GQ) and the simple-move masks rebuilt from it and its rays
+    // (ref_parent_split's keep), so neither is live across the loop
     auto each_move = [&](auto&& visit) {
-      if constexpr (BULK) ref_for_each_special<STM>(p, Fs, Ts, visit);
-      else ref_for_each_move<STM>(p, visit);
+      if constexpr (GQ) {
+        const Board pp = sh.board(otid(w));
+        u32 unused;
+        const u64 keep = ~(sh.rays(otid(w)) | ref_pawn_sensitive<1 - STM>(pp, unused));
+        const u64 occ = occupied(pp), own = STM ? pp.b0 : (occ & ~pp.b0);
+        ref_for_each_special<STM>(pp, own & keep, ~occ & keep, visit);
+      } else if constexpr (BULK) {
+        ref_for_each_special<STM>(p, Fs, Ts, visit);
+      } else {
+        ref_for_each_move<STM>(p, visit);
+      }
     };
     const u32 pl15 = otid(w) << 15;
     if (total <= CAP) {  // the norm: one window, no range checks
@@ -1171,15 +1290,15 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       const Cand ca = fetch(sh.slot[ra]);
       const Cand cb = fetch(lb ? sh.slot[rb] : 0u);
       consume(ca, true);
-      if (qn >= 64) drain64();
+      drain();
       consume(cb, lb);
-      if (qn >= 64) drain64();
+      drain();
     }
     for (; r0 < nslots; r0 += 256) {  // (DC_C2C_PAIR: at most one round left)
       const u32 ra = r0 + lane;
       const bool la = ra < nslots;
       consume(fetch(la ? sh.slot[ra] : 0u), la);
-      if (qn >= 64) drain64();
+      drain();
     }
   }
   // drain this wave's queue (par/att of the chunk are still in LDS)
@@ -1190,6 +1309,15 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     const u32 k = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2)) : 0u;
     add(e2 >> 15, k, live);
   }
+#if DC_C2C_DIAGQ
+  if (GQ && qnd) {
+    wave_lds_sync();
+    const bool live = lane < qnd;
+    const u32 e2 = live ? qd[lane] : 0u;
+    const u32 k = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_diag<STM>(sh, e2)) : 0u;
+    add(e2 >> 15, k, live);
+  }
+#endif
   tag_hist_add(sh.hist, tag0, acc, true);
   __syncthreads();  // par/att/ptag/slot reused by the next group
 }

@@ -262,6 +262,84 @@ __device__ __forceinline__ u32 ref_count_nonpawn(const Board& b, u64& att) {
   return c;
 }
 
+// ref_count_nonpawn with the slider groups kept apart for the group-wise
+// recount (c2c_diag): also `orth` = the orthogonal rays plus the orthogonal
+// sliders themselves (a move touching it changes that group's count) and
+// `diag` = the diagonal group's move count.
+template <int SIDE>
+__device__ __forceinline__ u32 ref_count_nonpawn_g(const Board& b, u64& att, u64& orth, u32& diag) {
+  const Sides s = sides<SIDE>(b);
+  const u64 no = s.notown, n = s.N, e = s.empty;
+  // the king first: its several-kings branch would otherwise split a block
+  // holding all eight knight shifts live (spills at the 128-VGPR budget)
+  u32 c = king_moves(s.K, no);
+  c += pc(and3(sh<17>(n), kNotA, no)) + pc(and3(sh<15>(n), kNotH, no));
+  c += pc(and3(sh<10>(n), kNotAB, no)) + pc(and3(sh<6>(n), kNotGH, no));
+  c += pc(and3(sh<-6>(n), kNotAB, no)) + pc(and3(sh<-10>(n), kNotGH, no));
+  c += pc(and3(sh<-15>(n), kNotA, no)) + pc(and3(sh<-17>(n), kNotH, no));
+  asm volatile("" : "+v"(c));  // the leaper terms reduced here, not sunk past the fills
+  const u64 a0 = ray_attacks<8, kAll>(s.O, e), a1 = ray_attacks<-8, kAll>(s.O, e);
+  const u64 a2 = ray_attacks<1, kNotA>(s.O, e), a3 = ray_attacks<-1, kNotH>(s.O, e);
+  const u64 a4 = ray_attacks<9, kNotA>(s.D, e), a5 = ray_attacks<-9, kNotH>(s.D, e);
+  const u64 a6 = ray_attacks<7, kNotH>(s.D, e), a7 = ray_attacks<-7, kNotA>(s.D, e);
+  c += pc(a0 & no) + pc(a1 & no) + pc(a2 & no) + pc(a3 & no);
+  diag = pc(a4 & no) + pc(a5 & no) + pc(a6 & no) + pc(a7 & no);
+  const u64 ao = bop3<0xFE>(a0, a1, a2) | a3;
+  orth = ao | s.O;
+  att = bop3<0xFE>(ao, bop3<0xFE>(a4, a5, a6), a7);
+  return c + diag;
+}
+
+// Knight and king attack sets of one square: the pattern around c3 / b2
+// shifted to s, the files a shift wraps into masked (king_moves' trick).
+__device__ __forceinline__ u64 knight_att_sq(int s) {
+  constexpr u64 kAtC3 = 0x0000000A1100110Aull;  // b1 d1 a2 e2 a4 e4 b5 d5 around c3 (18)
+  const u64 a = s >= 18 ? (kAtC3 << (s - 18)) : (kAtC3 >> (18 - s));
+  const int f = s & 7;
+  return a & (f <= 1 ? kNotGH : (f >= 6 ? kNotAB : kAll));
+}
+__device__ __forceinline__ u64 king_att_sq(int s) {
+  constexpr u64 kAtB2 = 0x0000000000070507ull;
+  const u64 a = s >= 9 ? (kAtB2 << (s - 9)) : (kAtB2 >> (9 - s));
+  const int f = s & 7;
+  return a & (f == 0 ? kNotH : (f == 7 ? kNotA : kAll));
+}
+
+// count_O of the child P∘(f -> t) (the other side's move; O = SIDE to move in
+// the child) when O's orthogonal group is unchanged (f, t off `orth` of
+// ref_count_nonpawn_g): from the parent's base (O's knight/king/slider moves)
+// and diag (its diagonal group's share),
+//   count = base - diag + diag group in the child + O's pawns in the child
+//           + [capture] (O's knights/kings attacking t, now an enemy square,
+//              minus the captured knight's or king's own moves).
+// Knights and kings see only the own/not-own status of their targets, which a
+// move changes at t alone (and only by a capture); the pawn terms and the
+// diagonal fills are recomputed on the child's occupancy.
+template <int SIDE>
+__device__ __forceinline__ u32 ref_count_child_diag(const Board& b, int f, int t, u32 base_minus_diag) {
+  typedef PawnDir<SIDE> PD;
+  const u64 occ = occupied(b);
+  const u64 bf = 1ull << f, bt = 1ull << t;
+  const u64 own0 = SIDE ? b.b0 : (occ & ~b.b0);
+  const u64 own = own0 & ~bt;                 // O's pieces in the child
+  const u64 occc = bop3<0xBA>(occ, bf, bt);   // (occ & ~f) | t
+  const u64 e = ~occc, no = ~own, enemy = occc ^ own;
+  const u64 D = and3(own, b.b3, b.b1);
+  u32 c = base_minus_diag;
+  c += pc(ray_moves<9, kNotA>(D, e, no)) + pc(ray_moves<-9, kNotH>(D, e, no));
+  c += pc(ray_moves<7, kNotH>(D, e, no)) + pc(ray_moves<-7, kNotA>(D, e, no));
+  const u64 P = and_andn(own, b.b1, b.b2 | b.b3);
+  const u64 push1 = sh<PD::F>(P) & e;
+  c += pc(push1) + pc(and3(sh<PD::F>(push1), PD::ROW_DBL, e));
+  c += pc(and3(sh<PD::CW>(P), kNotH, enemy)) + pc(and3(sh<PD::CE>(P), kNotA, enemy));
+  const u64 kn = knight_att_sq(t), kg = king_att_sq(t);
+  const u64 N = and_andn(own, b.b2, b.b1 | b.b3), K = and_andn(own, b.b1 & b.b2, b.b3);
+  const u32 xk = (u32)(((b.b1 >> t) & 1) | (((b.b2 >> t) & 1) << 1) | (((b.b3 >> t) & 1) << 2));
+  const u32 gain = pc(kn & N) + pc(kg & K);
+  const u32 lost = xk == KC_N ? pc(kn & ~own0) : (xk == KC_K ? pc(kg & ~own0) : 0u);
+  return ((own0 >> t) & 1) ? c + gain - lost : c;
+}
+
 // Pawn moves of SIDE in the child reached from `b` by the other side's quiet
 // move f -> t (f occupied by the mover, t empty): the pawn terms of ref_count
 // on the child's occupancy, without making the child.
@@ -355,13 +433,15 @@ __device__ __forceinline__ void ray_attacks2(u64 g1, u64 g2, u64 empty, u64& r1,
 // live across them (CSE) and spilled 184 B per lane -- 0.9 GB of scratch
 // traffic per perft(7) launch (rocprofv3 FETCH_SIZE).
 struct ParentSplit {
-  u64 att, Fs, Ts;
-  u32 base, pawn_o, n_total, n_simple;
+  u64 att, Fs, Ts, orth;
+  u32 base, pawn_o, n_total, n_simple, diag;
 };
 
-template <int STM>
+// GROUPS: also orth/diag (ref_count_nonpawn_g) for the group-wise recount.
+template <int STM, bool GROUPS = false>
 __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r) {
-  r.base = ref_count_nonpawn<1 - STM>(b, r.att);
+  if constexpr (GROUPS) r.base = ref_count_nonpawn_g<1 - STM>(b, r.att, r.orth, r.diag);
+  else r.base = ref_count_nonpawn<1 - STM>(b, r.att);
   const u64 keep = ~(r.att | ref_pawn_sensitive<1 - STM>(b, r.pawn_o));
   const Sides s = sides<STM>(b);
   const u64 Fs = s.own & keep, Ts = s.empty & keep, no = s.notown;

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <type_traits>
 
 #define SECP_HD __host__ __device__ __forceinline__
 
@@ -815,6 +816,19 @@ SECP_HD int booth_digit(const u32 (&m)[4], int w) {
   return (int)(lo + below) - (int)((lo >> (W - 1)) << W);
 }
 
+// f(integral_constant<int, I>) for I = B, B + S, ... while I != E: a loop whose
+// index is a compile-time constant in every iteration.  `#pragma unroll` did
+// not unroll the table build (gej_add_ge's special-case branches): X/Y/Z, the
+// prefix products and the table were then indexed by an SGPR and lived in
+// scratch (992 B/lane, most of k_verify_tx's HBM traffic).
+template <int B, int E, int S = 1, class F>
+SECP_HD void static_for(F&& f) {
+  if constexpr (B != E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + S, E, S>(f);
+  }
+}
+
 template <int W>
 SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge* gtab) {
   constexpr int K = 1 << (W - 1);
@@ -838,25 +852,27 @@ SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge*
       Y[1] = t.y;
       Z[1] = t.z;
     }
-#pragma unroll
-    for (int i = 2; i < K; ++i) {
+    static_for<2, K>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
       gej_add_ge(a, t, q);
       X[i] = a.x;
       Y[i] = a.y;
       Z[i] = a.z;
       t = a;
-    }
+    });
     // batch inversion of Z[0..K): prefix products, one inversion, back-substitution
     Fe c[K];
     c[0] = Z[0];
-#pragma unroll
-    for (int i = 1; i < K; ++i) fe_mul(c[i], c[i - 1], Z[i]);
+    static_for<1, K>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      fe_mul(c[i], c[i - 1], Z[i]);
+    });
     Fe inv;
     fe_inv(inv, c[K - 1]);
-#pragma unroll
-    for (int i = K - 1; i >= 0; --i) {
+    static_for<K - 1, -1, -1>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
       Fe zi;
-      if (i > 0) {
+      if constexpr (i > 0) {
         fe_mul(zi, inv, c[i - 1]);
         fe_mul(inv, inv, Z[i]);
       } else {
@@ -867,7 +883,7 @@ SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge*
       fe_mul(zi3, zi2, zi);
       fe_mul(tab[i].x, X[i], zi2);
       fe_mul(tab[i].y, Y[i], zi3);
-    }
+    });
   }
   Fe beta;
   fe_beta(beta);
@@ -884,11 +900,11 @@ SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge*
       if (d) {
         const int ad = d < 0 ? -d : d;
         Ge p = tab[0];
-#pragma unroll
-        for (int i = 1; i < K; ++i) {  // select, not an index: the table stays in VGPRs
+        static_for<1, K>([&](auto ic) {  // select, not an index: the table stays in VGPRs
+          constexpr int i = decltype(ic)::value;
           sel8(p.x.v, ad == i + 1, tab[i].x.v, p.x.v);
           sel8(p.y.v, ad == i + 1, tab[i].y.v, p.y.v);
-        }
+        });
         if (h) fe_mul(p.x, p.x, beta);
         if ((d < 0) != (h ? n2 : n1)) fe_neg(p.y, p.y);
         Gej t;
@@ -899,7 +915,12 @@ SECP_HD void ecmult_w(Gej& r, const Ge& q, const Sc& u2, const Sc& u1, const Ge*
   }
 #pragma unroll
   for (int i = 0; i < kGTabRows; ++i) {
-    const u32 b = (u1.v[i >> 2] >> (8 * (i & 3))) & 255u;
+    // (the loop stays rolled: the limb by select, not u1.v[i >> 2], which
+    // would put u1 in scratch)
+    const int l = i >> 2;
+    u32 limb = u1.v[0];
+    static_for<1, 8>([&](auto ic) { limb = l == decltype(ic)::value ? u1.v[decltype(ic)::value] : limb; });
+    const u32 b = (limb >> (8 * (i & 3))) & 255u;
     if (b) {
       const Ge g = gtab[256 * i + b];
       Gej t;

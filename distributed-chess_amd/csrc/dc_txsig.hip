@@ -25,7 +25,7 @@ namespace dc {
 
 constexpr u32 kTxThreads = 128;
 #ifndef DC_TX_MINW
-#define DC_TX_MINW 3  // waves per SIMD the register budget allows (168 VGPRs)
+#define DC_TX_MINW 2  // waves per SIMD: 2 (248 VGPRs) is spill-free; 3 (168) spilled 452 B/lane
 #endif
 
 __global__ __launch_bounds__(256) void k_secp_gtab(secp::Ge* __restrict__ gtab) {

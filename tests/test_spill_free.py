@@ -3,7 +3,8 @@ gfx950 code objects).  Round 2's only wrong perft counts came from final-stage
 builds that spilled registers to scratch at 4 waves/SIMD (DESIGN.md section
 7); since round 3 every REF perft, replay and validation kernel is built
 spill-free, and this test keeps it so: .private_segment_fixed_size == 0 in the
-AMDGPU metadata of every such kernel."""
+AMDGPU metadata of every such kernel.  The signature kernel joined them late in
+round 3 (its Q table was SGPR-indexed in scratch; now 248 VGPRs, 0 B)."""
 import os
 import re
 import shutil
@@ -17,7 +18,7 @@ import dchess
 LLVM = "/opt/rocm/lib/llvm/bin"
 # mangled-name fragments of the kernels that must stay spill-free
 MUST = ("k_count3c", "k_count2c", "k_perft_dfs", "k_replay_ref4", "k_validate_ref", "k_apply_ref",
-        "k_gen_games_ref", "RefRules")
+        "k_gen_games_ref", "RefRules", "k_verify_tx")
 
 
 def kernel_scratch():

@@ -26,6 +26,7 @@ flags_of() {
     rec) echo "-DDC_C2C_REC=1" ;;                          # 48-byte parent records (one LDS address per thread)
     soa_otid) echo "-DDC_C2C_REC=0 -DDC_C2C_SOA=1" ;;      # the soa layout built from the spill-free (otid) source
     soa_r2) echo "-DDC_C2C_SOA=1" ;;                       # round 2's failing build, rebuilt from commit 3d8df08
+    nodq) echo "-DDC_C2C_DIAGQ=0" ;;                       # round-3 v2 final stage: every non-quiet child recounted in full
     *) echo "unknown variant $1" >&2; exit 1 ;;
   esac
 }
