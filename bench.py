@@ -294,7 +294,11 @@ def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
                           (SQ_ACTIVE_INST_VALU x 64)): lane-ops actually done;
       frac_int          = rate x W_int / peak with W_int = (SQ_INSTS_VALU_INT32 +
                           SQ_INSTS_VALU_INT64) x 64 / units: SURVEY §8d's and
-                          BASELINE.md §3's INT32 VALU fraction.
+                          BASELINE.md §3's INT32 VALU fraction;
+      valu_busy         = rocprof VALUBusy / 100 (PMC pass, same kernel): the
+                          VALU pipes' busy cycles, where half-rate ops (64-bit
+                          shifts, v_bcnt, VOP3 selects) count twice -- the
+                          pipe occupancy the issue fraction understates.
     W_frozen (the first parity-passing kernel's W) is reported
     beside them as the algorithmic gain W_frozen / W, not as a roofline."""
     w = None
@@ -322,7 +326,7 @@ def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
         if w_int is not None:
             roof[f"W_int_lane_ops_per_{unit_name}"] = w_int
             roof["frac_int"] = rate * w_int / peak
-        for k in ("lds_conflict_per_lds_cycle", "wait_frac", "salu_per_valu"):
+        for k in ("lds_conflict_per_lds_cycle", "wait_frac", "salu_per_valu", "valu_busy"):
             if k in pmc_rec:
                 roof[k] = pmc_rec[k]
     return roof
@@ -613,7 +617,7 @@ def cpu_txsig(threads):
                       "core; the reference's libsecp256k1 could not be built here"}
 
 
-LEGS = ("perft", "perft6", "perft8", "fide7", "fidesuite", "replay", "hash", "tx", "latency")
+LEGS = ("perft", "perft6", "perft8", "perft9", "fide7", "fidesuite", "replay", "hash", "tx", "latency")
 # Published FIDE perft counts (chessprogramming wiki; tests/golden/oracle_golden.json perft_fide),
 # the C2/C3/C5 configurations under standard rules, which the reference cannot compute.
 _OG = json.load(open(os.path.join(REPO, "tests", "golden", "oracle_golden.json")))["perft_fide"]
@@ -659,10 +663,10 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
 
 
 def perft8_leg(eng, d, args, pos):
-    """REF perft(startpos, 8) through K4 (k_perft_dfs: per-lane DFS below the ply-5
-    frontier), timed like the headline and checked against the committed golden
-    (tests/golden/ref_deep.json, fastcpu).  Secondary: the north star's explicit
-    per-lane-stack path."""
+    """REF perft(startpos, 8): BFS to ply 5, ply 6 as 64-bit move words and the
+    fused three-ply final stage (k_level_moves + k_count3c, as the headline one
+    level deeper), timed like the headline and checked
+    against the committed golden (tests/golden/ref_deep.json, fastcpu)."""
     deep = os.path.join(REPO, "tests", "golden", "ref_deep.json")
     want = json.load(open(deep)).get("startpos_d8", {}).get("total") if os.path.exists(deep) else None
     if want is not None:
@@ -674,16 +678,44 @@ def perft8_leg(eng, d, args, pos):
     perft_step(eng, d, args, pos, 8)
     d.sync()
     eng.set_profiling(False)
+    ks = {k: eng.kernel_stats(k) for k in ("count2", "dfs")}
+    out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
+           "workload": "perft(startpos, 8) RULES_REF: BFS to ply 5, ply 6 as 64-bit move words, three-ply fused "
+                       "final stage (k_count3c)", "scaling": "strong", "leaves_per_step": leaves // steps,
+           "parity": "golden (fastcpu, tests/golden/ref_deep.json)" if want is not None else "no golden",
+           "path": "k4" if ks["dfs"]["launches"] else "fused"}
+    if ks["count2"]["launches"]:
+        out["roofline"] = roofline(ks, 8, d.world)
+    return out
+
+
+def perft9_leg(eng, d, args, pos):
+    """REF perft(startpos, 9) through K4 (k_perft_dfs: BFS to ply 5, then a
+    per-lane DFS with an explicit stack over 2 plies and the two-ply bulk final
+    stage per reached node): the north star's per-lane-stack path (SURVEY §2
+    K4), checked against the committed golden every step (2,597,923,551,373)."""
+    deep = os.path.join(REPO, "tests", "golden", "ref_deep.json")
+    want = json.load(open(deep)).get("startpos_d9", {}).get("total") if os.path.exists(deep) else None
+    if want is not None:
+        REF_STARTPOS[9] = want
+    steps = 2
+    leaves, dt = timed_perft(eng, d, args, pos, 9, steps, 1)
+    eng.reset_stats()
+    eng.set_profiling(True)
+    perft_step(eng, d, args, pos, 9)
+    d.sync()
+    eng.set_profiling(False)
     k = eng.kernel_stats("dfs")
     out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
-           "workload": "perft(startpos, 8) RULES_REF: BFS to ply 5, then K4 per-lane DFS (1 ply) + two-ply bulk final "
-                       "stage", "scaling": "strong", "leaves_per_step": leaves // steps,
+           "workload": "perft(startpos, 9) RULES_REF: BFS to ply 5, then K4 per-lane DFS (2 plies) + two-ply bulk "
+                       "final stage", "scaling": "strong", "leaves_per_step": leaves // steps,
            "parity": "golden (fastcpu, tests/golden/ref_deep.json)" if want is not None else "no golden",
            "dfs_kernel_ms": k["total_ms"] / max(k["launches"], 1)}
-    rec = _pmc("dfs_d8") if d.world == 1 else None
+    rec = _pmc("dfs_d9") if d.world == 1 else None
     if rec and k["launches"]:
         rate = k["units"] / max(k["launches"], 1) / (out["dfs_kernel_ms"] / 1e3)
         out["roofline"] = valu_roof("k_perft_dfs", rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
+        out["roofline"]["kernel_leaves_per_s"] = rate
     return out
 
 
@@ -706,7 +738,7 @@ def main():
         if args.no_perft:
             legs -= {"perft"}
         if args.profile_only:  # rocprof passes: headline (or replay + tx with --no-perft) only
-            legs -= {"perft6", "perft8", "fide7", "fidesuite", "hash", "latency"}
+            legs -= {"perft6", "perft8", "perft9", "fide7", "fidesuite", "hash", "latency"}
             if not args.no_perft:
                 legs -= {"tx"}
         if args.no_replay or args.games <= 0:
@@ -718,7 +750,7 @@ def main():
         if args.depth == 6:
             legs -= {"perft6"}
     # ------------------------------------------------- perft (headline: depth 7)
-    p6 = p8 = None
+    p6 = p8 = p9 = None
     leaves, dt, ks = 0, 0.0, None
     if "perft" in legs:
         leaves, dt = timed_perft(eng, d, args, pos, args.depth, args.steps, args.warmup)
@@ -731,6 +763,8 @@ def main():
               "scaling": "strong"}
     if "perft8" in legs:
         p8 = perft8_leg(eng, d, args, pos)
+    if "perft9" in legs:
+        p9 = perft9_leg(eng, d, args, pos)
     f7 = fs = None
     if "fide7" in legs:  # BASELINE configs[4]'s perft(startpos, 7) under standard rules
         f7 = fide_leg(eng, d, args, "perft(startpos, 7) RULES_FIDE", 7, ("startpos",), "fide_d7")
@@ -774,6 +808,8 @@ def main():
         line["kernels_ms_per_step"] = {k: v["total_ms"] / args.steps for k, v in ks.items()}
     if p8 is not None:
         line["perft8"] = p8
+    if p9 is not None:
+        line["perft9"] = p9
     if p6 is not None:
         line["perft6"] = p6
     if f7 is not None:

@@ -123,11 +123,11 @@ struct dc_ctx {
   uint32_t io_seq = 0;                   // last completion flag value published into host_io->done
   // The last perft launch sequence, captured as a hipGraph (see perft_run).
   struct PerftKey {
-    u32 rules, depth, split, shard, n_shards, stm;
+    u32 rules, depth, split, shard, n_shards, stm, k4;
     uint64_t epoch;
     bool operator==(const PerftKey& o) const {
       return rules == o.rules && depth == o.depth && split == o.split && shard == o.shard &&
-             n_shards == o.n_shards && stm == o.stm && epoch == o.epoch;
+             n_shards == o.n_shards && stm == o.stm && k4 == o.k4 && epoch == o.epoch;
     }
   } pkey{};
   hipGraphExec_t pgraph = nullptr;
@@ -159,6 +159,7 @@ struct dc_ctx {
   DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
   DBuf<u32> move_words;  // k_count3c: the final stage's parents as move words below their grandparents
+  DBuf<u64> move_words64;  // ... as 64-bit words (REF perft(8): more than 2^20 grandparents)
   DBuf<u32> top_words;   // k_expand_top's last ply as move words (k_make_count makes it)
   // transaction-signature check: staged strings / offsets / actions / turns,
   // and the G table (built on first use)
@@ -189,6 +190,7 @@ struct dc_ctx {
     top_words.release();
     move_words.release();
     dfs_stack.release();
+    move_words64.release();
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (rgraph) (void)hipGraphExecDestroy(rgraph);
     if (res_host) (void)hipHostFree(res_host);
@@ -1037,6 +1039,15 @@ constexpr u64 kNodeBytes = sizeof(Board) + 2 * sizeof(uint16_t);
 // Ply 5 of startpos is 4.9M nodes (196 MB); a typical middlegame ply 5 stays
 // within the speculative budget (Kiwipete's is 193M nodes, 6.6 GB).
 constexpr u32 kDfsFrontier = 5;
+// REF perft(8) takes the fused final stage from ply 5 instead (k_level_moves
+// + k_count3c with 64-bit move words: startpos ply 6 is 120M words, 0.96 GB)
+// while the words fit this capacity; a larger ply 6 (or DCHESS_PERFT_K4=1 in
+// the environment, for tests) goes through K4 from ply 5.
+constexpr u64 kWideWordsMax = 1ull << 29;  // 4.3 GB of words
+bool perft_k4_forced() {
+  const char* e = std::getenv("DCHESS_PERFT_K4");
+  return e && e[0] == '1';
+}
 
 int ensure_level(dc_ctx* c, int b, u64 n, bool fide) {
   const size_t want = std::max<u64>(n, 1);
@@ -1099,10 +1110,12 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
+  // REF perft(8): ply 6 as 64-bit move words below ply 5 (see kWideWordsMax)
+  const bool wide = !fide && depth == kDfsFrontier + 3 && !perft_k4_forced();
   // REF beyond ply kDfsFrontier: K4 walks the last Ldfs plies above the final
   // stage per lane (k_perft_dfs) instead of materialising those levels
   u32 Ldfs = 0;
-  if (!fide && depth >= 3 && F > kDfsFrontier) {
+  if (!fide && depth >= 3 && F > kDfsFrontier && !wide) {
     Ldfs = F - kDfsFrontier;
     F = kDfsFrontier;
     if (Ldfs > 3) return DC_EUNSUPPORTED;
@@ -1148,6 +1161,10 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   // Capacity of level L + 1 (and the node guard of level L) in speculative
   // mode: the move-word level of the fused final stage, else a board level.
   auto spec_cap = [&](u32 lvl, u64 n_lvl, u64* guard) -> u64 {
+    if (fused3 && wide && lvl + 1 == F) {  // 64-bit words: no grandparent limit
+      *guard = 0;
+      return std::min<u64>(n_lvl * kBranchBound, kWideWordsMax);
+    }
     if (fused3 && lvl + 1 == F) {
       *guard = dc::kMoveWordNodesMax;
       return std::min<u64>(std::min<u64>(n_lvl, dc::kMoveWordNodesMax) * kBranchBound, 0xFFFFFFFFull);
@@ -1231,9 +1248,10 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       e = read_range(c, L, &nb);
       if (e != DC_SUCCESS) return e;
     }
-    if (fused3 && L + 1 == F && (!exact || nb <= dc::kMoveWordNodesMax)) {
-      // one u32 move word per child; in speculative mode a grandparent level
-      // past kMoveWordNodesMax is flagged on the device (exact rerun)
+    if (fused3 && L + 1 == F && (!exact || wide || nb <= dc::kMoveWordNodesMax)) {
+      // one u32 move word per child (u64 when wide); in speculative mode a
+      // grandparent level past kMoveWordNodesMax (a word level past
+      // kWideWordsMax) is flagged on the device (exact rerun)
       u64 guard = 0;
       u64 cap_f = spec_cap(L, nb, &guard);
       e = count_and_scan(stm, exact ? ~0ull : cap_f, 0, exact ? 0 : guard, false);
@@ -1242,17 +1260,28 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
         *host_sync = true;
         e = read_range(c, L + 1, &cap_f);
         if (e != DC_SUCCESS) return e;
+        if (wide && cap_f > kWideWordsMax) {
+          // too many words for the fused stage: K4 from this level (ply 5)
+          Ldfs = F - L;
+          F = L;
+          break;
+        }
         if (cap_f > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
       }
-      HIP_TRY(c->move_words.ensure(std::max<u64>(cap_f, 1)));
+      if (wide) HIP_TRY(c->move_words64.ensure(std::max<u64>(cap_f, 1)));
+      else HIP_TRY(c->move_words.ensure(std::max<u64>(cap_f, 1)));
       HIP_TRY(c->timed("level_moves", 0, [&] {
-        return dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, cnt_buf[cb]->p,
-                                      c->chunk_base.p, c->move_words.p, cap_f);
+        return wide ? dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, cnt_buf[cb]->p,
+                                             c->chunk_base.p, c->move_words64.p, cap_f)
+                    : dc::launch_level_moves(c->stream, stm, c->nodes[buf].p, c->rng.p + L, nb, cnt_buf[cb]->p,
+                                             c->chunk_base.p, c->move_words.p, cap_f);
       }));
       c->last_final = "count2";
       HIP_TRY(c->timed("count2", 0, [&] {
-        return dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L, c->rng.p + L + 1,
-                                  c->move_words.p, c->res.p);
+        return wide ? dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L,
+                                         c->rng.p + L + 1, c->move_words64.p, c->res.p)
+                    : dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L,
+                                         c->rng.p + L + 1, c->move_words.p, c->res.p);
       }));
       return DC_SUCCESS;
     }
@@ -1331,7 +1360,8 @@ static bool perft_graphs_enabled() {
 int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
               uint32_t n_shards, bool exact, dc::PerftResult* out) {
   const bool graphable = !exact && !c->profiling && perft_graphs_enabled();
-  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
+  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
+                       g_alloc_epoch.load()};
   if (graphable && c->pgraph && c->pkey == key) {
     int e = write_root_host(c, pos);
     if (e != DC_SUCCESS) return e;
@@ -1439,7 +1469,8 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
   if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
   if (n_runs == 0) return DC_SUCCESS;
   HIP_TRY(c->rcur.ensure(1));  // before the key: an allocation moves the epoch
-  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, g_alloc_epoch.load()};
+  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
+                       g_alloc_epoch.load()};
   const bool graphable = !c->profiling && perft_graphs_enabled();
   if (!c->root_host || !(graphable && c->rgraph && c->rkey == key)) {
     // a plain run (host sync) sizes the buffers and stages the root; then the

@@ -53,7 +53,11 @@ __device__ __forceinline__ u64 sh(u64 x) {
   if constexpr (S > 0) r = x << S;
   else if constexpr (S < 0) r = x >> -S;
 #else
-  if constexpr (S > 0) asm(DC_SHL_ASM : "=v"(r) : "i"(S), "v"(x));
+  // |S| >= 32 (the fills' 4 x 8 and 4 x 9 steps): one half moves, so a 32-bit
+  // shift (S = 32: a register copy) instead of the half-rate 64-bit one
+  if constexpr (S >= 32) r = (u64)((u32)x << (S - 32)) << 32;
+  else if constexpr (S <= -32) r = (u64)((u32)(x >> 32) >> (-S - 32));
+  else if constexpr (S > 0) asm(DC_SHL_ASM : "=v"(r) : "i"(S), "v"(x));
   else if constexpr (S < 0) asm(DC_SHR_ASM : "=v"(r) : "i"(-S), "v"(x));
 #endif
   else r = x;

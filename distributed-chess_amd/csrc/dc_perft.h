@@ -95,6 +95,12 @@ hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const
                               const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap);
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
                           const Range* rng_ch, const u32* mw, PerftResult* res);
+// The same with u64 words {grandparent index << 12 | f | t << 6} (no 2^20
+// grandparent limit): REF perft(8)'s final stage below ply 5.
+hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
+                              const u32* counts, const u64* chunk_base, u64* mw, u64 mw_cap);
+hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
+                          const Range* rng_ch, const u64* mw, PerftResult* res);
 
 // K4 (REF): per-lane DFS over L plies below the frontier level `rng` (1 <= L <= 3),
 // each level-L node bulk-counted over the last two plies (perft depth = frontier

@@ -613,10 +613,12 @@ struct MwShared {
   u64 wsum[4];
 };
 
-template <int STM>
+// W: u32 words (grandparent index < 2^20) or u64 words (perft(8): the ply-5
+// grandparents of startpos are 4.9M).
+template <int STM, class W = u32>
 __global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ nodes, const Range* __restrict__ rng,
                                                      const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
-                                                     u32* __restrict__ mw, u64 cap) {
+                                                     W* __restrict__ mw, u64 cap) {
   __shared__ MwShared sh;
   const u32 tid = threadIdx.x, g = tid >> 6, lane = lane_id();
   const u64 lo = rng->lo, hi = rng->hi;
@@ -674,7 +676,7 @@ __global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ n
         const u64 o = base_out + wb + r;
         if (o < cap) {  // words beyond cap are dropped (the level is flagged)
           const u32 e = sh.slot[r];
-          mw[o] = ((u32)(c * kChunk + (e >> 12)) << 12) | (e & 0xFFFu);
+          mw[o] = ((W)(c * kChunk + (e >> 12)) << 12) | (W)(e & 0xFFFu);
         }
       }
     }
@@ -1420,10 +1422,10 @@ constexpr u32 kMoveWordNodes = 1u << 20;  // grandparent index field of a move w
 // speculative bound) is flagged by the scan that sizes its children
 // (k_chunk_scan's guard): the children's Range is empty and
 // the host reruns in exact mode, which takes the k_level_write path.
-template <int STM_G, u32 CAP, int MINW = 4>
+template <int STM_G, u32 CAP, int MINW = 4, class W = u32>
 __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, const Range* __restrict__ rng_ch,
-                                                 const u32* __restrict__ mw, u64* __restrict__ divide,
+                                                 const W* __restrict__ mw, u64* __restrict__ divide,
                                                  u32* __restrict__ next_group) {
   __shared__ C2cShared<CAP> sh;
   tag_hist_init(sh.hist);
@@ -1451,11 +1453,12 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
     Board ch{0, 0, 0, 0};
     u32 tag = 0;
     if (valid) {
-      const u32 e = mw[i];
-      const u64 g = lo + (e >> 12);
+      const W e = mw[i];
+      const u64 g = lo + (u64)(e >> 12);
       ch = load_board(nodes, g);
       tag = tags[g];
-      ref_make(ch, (int)(e & 63), (int)((e >> 6) & 63));
+      const u32 mv = (u32)e;
+      ref_make(ch, (int)(mv & 63), (int)((mv >> 6) & 63));
     }
     c2c_group<1 - STM_G, CAP>(sh, valid, ch, tag, divide, wave);
 #if DC_C3C_LOG
@@ -1838,13 +1841,22 @@ hipError_t launch_perft_dfs(hipStream_t st, int stm_parent, u32 L, const Board* 
   return hipGetLastError();
 }
 
-hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
-                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap) {
+template <class W>
+static hipError_t level_moves_w(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
+                                const u32* counts, const u64* chunk_base, W* mw, u64 mw_cap) {
   // words beyond mw_cap are dropped (a flagged level is never read)
-  auto k = stm ? k_level_moves<1> : k_level_moves<0>;
+  auto k = stm ? k_level_moves<1, W> : k_level_moves<0, W>;
   hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, grid_for(std::min<u64>(n_bound, kMoveWordNodes) * 4, kChunk))),
                      dim3(256), 0, st, nodes, rng, counts, chunk_base, mw, mw_cap);
   return hipGetLastError();
+}
+hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
+                              const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap) {
+  return level_moves_w(st, stm, nodes, rng, n_bound, counts, chunk_base, mw, mw_cap);
+}
+hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
+                              const u32* counts, const u64* chunk_base, u64* mw, u64 mw_cap) {
+  return level_moves_w(st, stm, nodes, rng, n_bound, counts, chunk_base, mw, mw_cap);
 }
 
 // k_count3c's special-child slots per parent and waves per SIMD (VGPR budget);
@@ -1857,18 +1869,27 @@ constexpr u32 kC3cCap = kC2cCap;
 #ifndef DC_C3C_MINW
 #define DC_C3C_MINW 4
 #endif
-hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u32* mw, PerftResult* res) {
+template <class W>
+static hipError_t count3c_w(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
+                            const Range* rng_ch, const W* mw, PerftResult* res) {
   if (stm_g) {
-    auto k = k_count3c<1, kC3cCap, DC_C3C_MINW>;
+    auto k = k_count3c<1, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
                        res->divide, &res->next_chunk);
   } else {
-    auto k = k_count3c<0, kC3cCap, DC_C3C_MINW>;
+    auto k = k_count3c<0, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
                        res->divide, &res->next_chunk);
   }
   return hipGetLastError();
+}
+hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
+                          const Range* rng_ch, const u32* mw, PerftResult* res) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res);
+}
+hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
+                          const Range* rng_ch, const u64* mw, PerftResult* res) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res);
 }
 
 // Product: REF -> k_count2c (the bulk split), FIDE -> k_count2b<FideRules>.

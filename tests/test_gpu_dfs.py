@@ -1,8 +1,11 @@
 """K4 -- per-lane DFS perft (k_perft_dfs) -- on the GPU through libdchess.so.
 
-Under RULES_REF a perft deeper than 7 keeps its BFS levels at ply <= 5 and
+Under RULES_REF a perft deeper than 8 keeps its BFS levels at ply <= 5 and
 walks the remaining L = depth - 7 plies above the two-ply final stage per
-lane with an explicit stack.  Checked against
+lane with an explicit stack.  perft(8) takes the fused final
+stage below ply 5 with 64-bit move words (k_level_moves + k_count3c) and falls
+back to K4 (L = 1) when ply 6 is too large; DCHESS_PERFT_K4=1 forces K4 there,
+so both depth-8 paths are checked.  Checked against
   * fastcpu (oracle/fastcpu.cpp) on sparse positions at depths 8, 9 and 10
     (L = 1, 2, 3), computed in the test;
   * the committed startpos perft(8) divide (tests/golden/ref_deep.json,
@@ -30,8 +33,20 @@ SPARSE = [
 ]
 
 
+@pytest.fixture(params=["fused", "k4"])
+def d8_path(request, monkeypatch):
+    """The depth-8 path: the fused final stage below ply 5 (default) or K4."""
+    if request.param == "k4":
+        monkeypatch.setenv("DCHESS_PERFT_K4", "1")
+    else:
+        monkeypatch.delenv("DCHESS_PERFT_K4", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("fen,depth", SPARSE, ids=[f"d{d}-{i}" for i, (_, d) in enumerate(SPARSE)])
-def test_dfs_sparse_vs_fastcpu(engine, fen, depth):
+def test_dfs_sparse_vs_fastcpu(engine, fen, depth, d8_path):
+    if depth != 8 and d8_path == "fused":
+        pytest.skip("the path switch applies at depth 8 only")
     p = O.Pos.from_fen(fen)
     want, wdiv, wrm = O.fast_perft(p, depth, O.REF, threads=min(16, os.cpu_count() or 1))
     tot, div, rm = engine.perft(dchess.pos_from_fen(fen), depth)
@@ -39,15 +54,24 @@ def test_dfs_sparse_vs_fastcpu(engine, fen, depth):
     assert dict(zip(rm.tolist(), div.tolist())) == dict(zip(wrm.tolist(), wdiv.tolist()))
 
 
-def test_perft8_startpos_golden(engine):
+def test_perft8_startpos_golden(engine, d8_path):
     g = DEEP["startpos_d8"]
     tot, div, rm = engine.perft(dchess.startpos(), 8)
     assert tot == g["total"]
     assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+    assert engine.perft(dchess.startpos(), 8)[0] == g["total"]  # the captured graph's replay
+    engine.reset_stats()
+    engine.set_profiling(True)
+    try:
+        assert engine.perft(dchess.startpos(), 8)[0] == g["total"]
+        dfs, fin = engine.kernel_stats("dfs")["launches"], engine.kernel_stats("count2")["launches"]
+    finally:
+        engine.set_profiling(False)
+    assert (dfs, fin) == ((1, 0) if d8_path == "k4" else (0, 1))  # the path asked for ran
 
 
 @pytest.mark.parametrize("n_shards", [3, 8])
-def test_perft8_shards_sum(engine, n_shards):
+def test_perft8_shards_sum(engine, n_shards, d8_path):
     s = dchess.startpos()
     acc, t = None, 0
     for k in range(n_shards):
@@ -57,7 +81,7 @@ def test_perft8_shards_sum(engine, n_shards):
     assert t == DEEP["startpos_d8"]["total"]
 
 
-def test_perft8_repeat_device(engine):
+def test_perft8_repeat_device(engine, d8_path):
     s = dchess.startpos()
     W, runs = 258, 2
     buf = engine.alloc(runs * W * 8)

@@ -35,17 +35,19 @@ if has pmc; then
   # 4 counter passes over every leg's kernels (one bench process per pass),
   # then per-kernel records -> $O/pmc_latest.json (tools/pmc_summary.py)
   rm -rf $O/pmc_p*
-  P="--steps 8 --warmup 1 --no-cpu --replay-steps 2 --hash-steps 1 --tx-steps 1 --only perft,perft8,replay,hash,tx"
+  P="--steps 8 --warmup 1 --no-cpu --replay-steps 2 --hash-steps 1 --tx-steps 1 --only perft,perft8,perft9,replay,hash,tx"
   pass() {  # $1 counters, $2 tag
     step "pmc $2"
     timeout -s KILL 240 rocprofv3 --pmc $1 --output-format csv -d $O/pmc_$2 -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err
   }
   pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" p1 && \
   pass "FETCH_SIZE" p2 && pass "WRITE_SIZE" p3 && \
-  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" p4 || { tail $O/pmc.err; exit 5; }
+  pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" p4 && \
+  pass "VALUBusy" p5 || { tail $O/pmc.err; exit 5; }
   D8=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d8']['total'])")
+  D9=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d9']['total'])")
   python tools/pmc_summary.py $O --json $O/pmc_latest.json --source "rocprofv3 --pmc (4 passes), bench.py $P" \
-    --units "final_d7=k_count3c<=3282734510" --units "dfs_d8=k_perft_dfs<=$D8" \
+    --units "final_d7=k_count3c<0=3282734510" --units "final_d8=k_count3c<1=$D8" --units "dfs_d9=k_perft_dfs<=$D9" \
     --units "replay=k_replay_ref4=799999953" --units "gen_games=k_gen_games_ref=799999953" \
     --units "state_hash=k_state_hash_ref=1000000" --units "verify_tx=k_verify_tx=262144" > $O/pmc_summary.txt
 fi
@@ -58,8 +60,9 @@ if has fidepmc; then
     fpass() { local c=$1 t=$2; step "pmc $t"; timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err; }
     fpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" f1$leg && \
     fpass "FETCH_SIZE" f2$leg && fpass "WRITE_SIZE" f3$leg && \
-    fpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" f4$leg || { tail $O/pmc.err; exit 8; }
-    mkdir -p $O/$leg && mv $O/pmc_f[1-4]$leg $O/$leg/
+    fpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" f4$leg && \
+    fpass "VALUBusy" f5$leg || { tail $O/pmc.err; exit 8; }
+    mkdir -p $O/$leg && mv $O/pmc_f[1-5]$leg $O/$leg/
   done
   python tools/pmc_summary.py $O/fide7 --json $O/pmc_fide7.json --source "rocprofv3 --pmc (4 passes), bench.py --only fide7" \
     --units "fide_d7=k_count2b<dc::FideRules=3195901860" > $O/pmc_fide.txt

@@ -13,6 +13,8 @@ Per kernel record (units = the kernel's work units per dispatch, from --units):
                            (rocprof's VALUUtilization: active lanes per VALU op)
   lds_conflict_per_lds_cycle = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS
   wait_frac              = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
+  valu_busy              = rocprof's derived VALUBusy / 100: cycles the VALU pipes
+                           are busy (half-rate ops count twice) per available cycle
 bench.py turns these into fractions of the 78.6 T lane-op/s issue peak with the
 kernel's live HIP-event time.
 
@@ -65,6 +67,8 @@ def derived(c, units):
         r["lds_conflict_per_lds_cycle"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_ACTIVE_INST_LDS"]
     if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_INST_ANY" in c:
         r["wait_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
+    if "VALUBusy" in c:
+        r["valu_busy"] = c["VALUBusy"] / 100.0
     if c.get("SQ_INSTS_VALU") and "SQ_INSTS_SALU" in c:
         r["salu_per_valu"] = c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"]
     return r
