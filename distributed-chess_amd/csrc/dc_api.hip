@@ -1044,6 +1044,12 @@ constexpr u32 kDfsFrontier = 5;
 // while the words fit this capacity; a larger ply 6 (or DCHESS_PERFT_K4=1 in
 // the environment, for tests) goes through K4 from ply 5.
 constexpr u64 kWideWordsMax = 1ull << 29;  // 4.3 GB of words
+// (DCHESS_PERFT_WIDE_MAX lowers it, so a test can take the fallback on a small tree)
+u64 wide_words_max() {
+  const char* e = std::getenv("DCHESS_PERFT_WIDE_MAX");
+  const u64 v = e ? std::strtoull(e, nullptr, 10) : 0;
+  return v ? std::min<u64>(v, kWideWordsMax) : kWideWordsMax;
+}
 bool perft_k4_forced() {
   const char* e = std::getenv("DCHESS_PERFT_K4");
   return e && e[0] == '1';
@@ -1163,7 +1169,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   auto spec_cap = [&](u32 lvl, u64 n_lvl, u64* guard) -> u64 {
     if (fused3 && wide && lvl + 1 == F) {  // 64-bit words: no grandparent limit
       *guard = 0;
-      return std::min<u64>(n_lvl * kBranchBound, kWideWordsMax);
+      return std::min<u64>(n_lvl * kBranchBound, wide_words_max());
     }
     if (fused3 && lvl + 1 == F) {
       *guard = dc::kMoveWordNodesMax;
@@ -1260,7 +1266,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
         *host_sync = true;
         e = read_range(c, L + 1, &cap_f);
         if (e != DC_SUCCESS) return e;
-        if (wide && cap_f > kWideWordsMax) {
+        if (wide && cap_f > wide_words_max()) {
           // too many words for the fused stage: K4 from this level (ply 5)
           Ldfs = F - L;
           F = L;

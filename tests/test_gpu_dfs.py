@@ -70,6 +70,20 @@ def test_perft8_startpos_golden(engine, d8_path):
     assert (dfs, fin) == ((1, 0) if d8_path == "k4" else (0, 1))  # the path asked for ran
 
 
+def test_perft8_wide_overflow_falls_back_to_k4(monkeypatch):
+    """A ply 6 larger than the 64-bit word capacity: the speculative run is
+    flagged, the exact rerun sees the word count and takes K4 from ply 5
+    (capacity lowered through DCHESS_PERFT_WIDE_MAX on a fresh context)."""
+    monkeypatch.delenv("DCHESS_PERFT_K4", raising=False)
+    monkeypatch.setenv("DCHESS_PERFT_WIDE_MAX", "1000")
+    fen = SPARSE[0][0]
+    want, _, _ = O.fast_perft(O.Pos.from_fen(fen), 8, O.REF, threads=min(16, os.cpu_count() or 1))
+    eng = dchess.Engine(0)
+    eng.set_profiling(True)
+    assert eng.perft(dchess.pos_from_fen(fen), 8)[0] == want
+    assert eng.kernel_stats("dfs")["launches"] == 1
+
+
 @pytest.mark.parametrize("n_shards", [3, 8])
 def test_perft8_shards_sum(engine, n_shards, d8_path):
     s = dchess.startpos()
