@@ -690,32 +690,58 @@ def perft8_leg(eng, d, args, pos):
 
 
 def perft9_leg(eng, d, args, pos):
-    """REF perft(startpos, 9) through K4 (k_perft_dfs: BFS to ply 5, then a
-    per-lane DFS with an explicit stack over 2 plies and the two-ply bulk final
-    stage per reached node): the north star's per-lane-stack path (SURVEY §2
-    K4), checked against the committed golden every step (2,597,923,551,373)."""
+    """REF perft(startpos, 9), both ways, each checked against the committed
+    golden every step (2,597,923,551,373):
+      * default: ply 6 as boards and the fused three-ply final stage over
+        slices of 2^21 ply-6 nodes (k_level_moves + k_count3c with 64-bit
+        words); its roofline takes W from the perft(8)
+        PMC record (the same kernel body, 64-bit words);
+      * "k4": K4 (k_perft_dfs: BFS to ply 5, then a per-lane DFS with an
+        explicit stack over 2 plies and the two-ply bulk final stage), forced
+        with DCHESS_PERFT_K4=1 -- the north star's per-lane-stack path."""
     deep = os.path.join(REPO, "tests", "golden", "ref_deep.json")
     want = json.load(open(deep)).get("startpos_d9", {}).get("total") if os.path.exists(deep) else None
     if want is not None:
         REF_STARTPOS[9] = want
+
+    def run(steps):
+        leaves, dt = timed_perft(eng, d, args, pos, 9, steps, 1)
+        eng.reset_stats()
+        eng.set_profiling(True)
+        perft_step(eng, d, args, pos, 9)
+        d.sync()
+        eng.set_profiling(False)
+        return leaves, dt, {k: eng.kernel_stats(k) for k in ("count2", "dfs")}
+
     steps = 2
-    leaves, dt = timed_perft(eng, d, args, pos, 9, steps, 1)
-    eng.reset_stats()
-    eng.set_profiling(True)
-    perft_step(eng, d, args, pos, 9)
-    d.sync()
-    eng.set_profiling(False)
-    k = eng.kernel_stats("dfs")
+    leaves, dt, ks = run(steps)
+    parity = "golden (fastcpu, tests/golden/ref_deep.json)" if want is not None else "no golden"
     out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
-           "workload": "perft(startpos, 9) RULES_REF: BFS to ply 5, then K4 per-lane DFS (2 plies) + two-ply bulk "
-                       "final stage", "scaling": "strong", "leaves_per_step": leaves // steps,
-           "parity": "golden (fastcpu, tests/golden/ref_deep.json)" if want is not None else "no golden",
-           "dfs_kernel_ms": k["total_ms"] / max(k["launches"], 1)}
+           "workload": "perft(startpos, 9) RULES_REF: BFS to ply 6, fused three-ply final stage over slices of "
+                       "ply 6 (64-bit move words)", "scaling": "strong", "leaves_per_step": leaves // steps,
+           "parity": parity, "path": "k4" if ks["dfs"]["launches"] else "fused-sliced",
+           "final_kernel_ms": ks["count2"]["total_ms"]}
+    rec = _pmc("final_d8") if d.world == 1 else None
+    if rec and ks["count2"]["launches"] and ks["count2"]["total_ms"] > 0:
+        rate = (want or leaves // steps) / d.world / (ks["count2"]["total_ms"] / 1e3)
+        out["roofline"] = valu_roof("k_count3c", rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
+        out["roofline"]["kernel_leaves_per_s"] = rate
+        out["roofline"]["W_note"] = "W of the perft(8) record: the same kernel body with 64-bit words"
+    os.environ["DCHESS_PERFT_K4"] = "1"
+    try:
+        l4, dt4, ks4 = run(1)
+    finally:
+        del os.environ["DCHESS_PERFT_K4"]
+    k = ks4["dfs"]
+    k4 = {"value": l4 / dt4, "ms_per_step": 1e3 * dt4, "steps": 1, "parity": parity,
+          "workload": "K4: BFS to ply 5, per-lane DFS (2 plies) + two-ply bulk final stage",
+          "dfs_kernel_ms": k["total_ms"] / max(k["launches"], 1)}
     rec = _pmc("dfs_d9") if d.world == 1 else None
     if rec and k["launches"]:
-        rate = k["units"] / max(k["launches"], 1) / (out["dfs_kernel_ms"] / 1e3)
-        out["roofline"] = valu_roof("k_perft_dfs", rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
-        out["roofline"]["kernel_leaves_per_s"] = rate
+        rate = k["units"] / max(k["launches"], 1) / (k4["dfs_kernel_ms"] / 1e3)
+        k4["roofline"] = valu_roof("k_perft_dfs", rate, "leaf", W_COUNT2, rec, "valu_lane_ops_per_leaf")
+        k4["roofline"]["kernel_leaves_per_s"] = rate
+    out["k4"] = k4
     return out
 
 

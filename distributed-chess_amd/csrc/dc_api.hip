@@ -160,6 +160,8 @@ struct dc_ctx {
   DBuf<u64> bitmap, digests, stats5;
   DBuf<u32> move_words;  // k_count3c: the final stage's parents as move words below their grandparents
   DBuf<u64> move_words64;  // ... as 64-bit words (REF perft(8): more than 2^20 grandparents)
+  DBuf<dc::Range> slice_rng;  // the sliced final stage (REF perft(9)): one slice's node and word Ranges
+  DBuf<u32> slice_ctr;        // ... and its group counter
   DBuf<u32> top_words;   // k_expand_top's last ply as move words (k_make_count makes it)
   // transaction-signature check: staged strings / offsets / actions / turns,
   // and the G table (built on first use)
@@ -191,6 +193,8 @@ struct dc_ctx {
     move_words.release();
     dfs_stack.release();
     move_words64.release();
+    slice_rng.release();
+    slice_ctr.release();
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (rgraph) (void)hipGraphExecDestroy(rgraph);
     if (res_host) (void)hipHostFree(res_host);
@@ -1042,13 +1046,24 @@ constexpr u32 kDfsFrontier = 5;
 // REF perft(8) takes the fused final stage from ply 5 instead (k_level_moves
 // + k_count3c with 64-bit move words: startpos ply 6 is 120M words, 0.96 GB)
 // while the words fit this capacity; a larger ply 6 (or DCHESS_PERFT_K4=1 in
-// the environment, for tests) goes through K4 from ply 5.
+// the environment, for tests) goes through K4 from ply 5.  REF perft(9) builds
+// ply 6 as boards (startpos: 120M, 4.3 GB) and runs the fused stage over
+// slices of kSliceNodes grandparents (each slice's words fit the capacity:
+// 2^21 nodes x 256 moves); a ply 6 past kWideLevelBytes goes through K4.
 constexpr u64 kWideWordsMax = 1ull << 29;  // 4.3 GB of words
+constexpr u64 kSliceNodes = 1ull << 21;
+constexpr u64 kWideLevelBytes = 48ull << 30;
 // (DCHESS_PERFT_WIDE_MAX lowers it, so a test can take the fallback on a small tree)
 u64 wide_words_max() {
   const char* e = std::getenv("DCHESS_PERFT_WIDE_MAX");
   const u64 v = e ? std::strtoull(e, nullptr, 10) : 0;
   return v ? std::min<u64>(v, kWideWordsMax) : kWideWordsMax;
+}
+// (DCHESS_PERFT_WIDE_LEVEL_MAX lowers kWideLevelBytes the same way)
+u64 wide_level_bytes() {
+  const char* e = std::getenv("DCHESS_PERFT_WIDE_LEVEL_MAX");
+  const u64 v = e ? std::strtoull(e, nullptr, 10) : 0;
+  return v ? std::min<u64>(v, kWideLevelBytes) : kWideLevelBytes;
 }
 bool perft_k4_forced() {
   const char* e = std::getenv("DCHESS_PERFT_K4");
@@ -1111,13 +1126,19 @@ static bool fused3_enabled() {
 // copy.  *host_sync is set when a level size had to be read back on the host
 // (exact mode or a level beyond the speculative budget): such a sequence
 // depends on data and is never captured as a graph.
+// rcur (dc_perft_repeat_device): where the run's result goes; *copied is set
+// when the final stage stored it there itself (k_count3c's last block), else
+// the caller launches k_copy_result.
 int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
-                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true) {
+                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true,
+                  dc::ResultCursor* rcur = nullptr, bool* copied = nullptr) {
+  if (copied) *copied = false;
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
-  // REF perft(8): ply 6 as 64-bit move words below ply 5 (see kWideWordsMax)
-  const bool wide = !fide && depth == kDfsFrontier + 3 && !perft_k4_forced();
+  // REF perft(8) and (9): 64-bit move words below ply 5 or slices of ply 6 (see kWideWordsMax)
+  const bool wide = !fide && (depth == kDfsFrontier + 3 || depth == kDfsFrontier + 4) && !perft_k4_forced();
+  const bool sliced = wide && depth == kDfsFrontier + 4;
   // REF beyond ply kDfsFrontier: K4 walks the last Ldfs plies above the final
   // stage per lane (k_perft_dfs) instead of materialising those levels
   u32 Ldfs = 0;
@@ -1176,6 +1197,8 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       return std::min<u64>(std::min<u64>(n_lvl, dc::kMoveWordNodesMax) * kBranchBound, 0xFFFFFFFFull);
     }
     *guard = 0;
+    if (sliced && lvl + 2 == F)  // the sliced stage's grandparents (a lowered budget: tests)
+      return std::min(n_lvl * kBranchBound, std::min(kSpecBudget, wide_level_bytes()) / kNodeBytes);
     return std::min(n_lvl * kBranchBound, kSpecBudget / kNodeBytes);
   };
   // The target ply of k_expand_top is made on many CUs by k_make_count (it
@@ -1254,6 +1277,36 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       e = read_range(c, L, &nb);
       if (e != DC_SUCCESS) return e;
     }
+    if (fused3 && sliced && L + 1 == F) {
+      // words of the whole level are never stored: per slice of grandparents,
+      // k_level_moves writes that slice's words and k_count3c counts them
+      e = count_and_scan(stm, ~0ull, 0, 0, false);
+      if (e != DC_SUCCESS) return e;
+      const u64 cap_w = std::min<u64>(kSliceNodes * 256, kWideWordsMax);
+      HIP_TRY(c->move_words64.ensure(cap_w));
+      HIP_TRY(c->slice_rng.ensure(2));
+      HIP_TRY(c->slice_ctr.ensure(1));
+      const u64 n_slices = std::max<u64>((nb + kSliceNodes - 1) / kSliceNodes, 1);
+      c->last_final = "count2";
+      for (u64 k = 0; k < n_slices; ++k) {
+        const u64 s0 = k * kSliceNodes;
+        const bool last = k + 1 == n_slices;
+        HIP_TRY(dc::launch_wide_slice(c->stream, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, s0, kSliceNodes,
+                                      c->slice_rng.p, c->slice_ctr.p, c->res.p, cap_w));
+        HIP_TRY(c->timed("level_moves", 0, [&] {
+          return dc::launch_level_moves(c->stream, stm, c->nodes[buf].p + s0, c->slice_rng.p, kSliceNodes,
+                                        cnt_buf[cb]->p + s0, c->chunk_base.p + dc::chunks_for(s0), c->move_words64.p,
+                                        cap_w);
+        }));
+        HIP_TRY(c->timed("count2", 0, [&] {
+          return dc::launch_count3c(c->stream, stm, c->nodes[buf].p + s0, c->tags[buf].p + s0, c->slice_rng.p,
+                                    c->slice_rng.p + 1, c->move_words64.p, c->res.p, last ? rcur : nullptr,
+                                    c->slice_ctr.p);
+        }));
+      }
+      if (copied) *copied = rcur != nullptr;
+      return DC_SUCCESS;
+    }
     if (fused3 && L + 1 == F && (!exact || wide || nb <= dc::kMoveWordNodesMax)) {
       // one u32 move word per child (u64 when wide); in speculative mode a
       // grandparent level past kMoveWordNodesMax (a word level past
@@ -1285,10 +1338,11 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       c->last_final = "count2";
       HIP_TRY(c->timed("count2", 0, [&] {
         return wide ? dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L,
-                                         c->rng.p + L + 1, c->move_words64.p, c->res.p)
+                                         c->rng.p + L + 1, c->move_words64.p, c->res.p, rcur)
                     : dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L,
-                                         c->rng.p + L + 1, c->move_words.p, c->res.p);
+                                         c->rng.p + L + 1, c->move_words.p, c->res.p, rcur);
       }));
+      if (copied) *copied = rcur != nullptr;
       return DC_SUCCESS;
     }
     // Speculative mode never reads a level size back: the next level gets
@@ -1310,6 +1364,12 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       *host_sync = true;
       e = read_range(c, L + 1, &cap_next);
       if (e != DC_SUCCESS) return e;
+      if (sliced && L + 2 == F && cap_next * kNodeBytes > wide_level_bytes()) {
+        // the sliced stage's grandparent level would not fit: K4 from this level
+        Ldfs = F - L;
+        F = L;
+        break;
+      }
       if (cap_next > 0xFFFFFFFFull) return DC_EUNSUPPORTED;
     }
     e = ensure_level(c, buf ^ 1, cap_next, fide);
@@ -1489,10 +1549,10 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
       // (one host sync per level), each result still left on the device
       HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out)));
       for (u32 i = 0; i < n_runs; ++i) {
-        bool hs = false;
-        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs);
+        bool hs = false, copied = false;
+        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs, true, c->rcur.p, &copied);
         if (e != DC_SUCCESS) return e;
-        HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
+        if (!copied) HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
       }
       return DC_SUCCESS;
     }
@@ -1503,10 +1563,12 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
         c->rgraph = nullptr;
       }
       if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-        bool hs = false;
+        bool hs = false, copied = false;
         // the result copy is part of the graph: its destination is the cursor
-        int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
-        if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
+        int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false, c->rcur.p,
+                               &copied);
+        if (ce == DC_SUCCESS && !copied && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess)
+          ce = DC_EHIP;
         hipGraph_t g = nullptr;
         const hipError_t ee = hipStreamEndCapture(c->stream, &g);
         if (ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
@@ -1536,10 +1598,11 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
     } else {
-      bool host_sync = false;
-      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync);
+      bool host_sync = false, copied = false;
+      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync, true, c->rcur.p,
+                            &copied);
       if (e != DC_SUCCESS) return e;
-      HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
+      if (!copied) HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
     }
   }
   return DC_SUCCESS;

@@ -634,7 +634,9 @@ __global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ n
     const bool valid = i < hi;
     Board p{0, 0, 0, 0};
     if (valid) p = load_board(nodes, i);
-    const u64 cbase = chunk_base[c];
+    // (relative to chunk_base[0]: 0 for a whole level, the slice's first word
+    // for a slice of one, perft_enqueue's sliced final stage)
+    const u64 cbase = chunk_base[c] - chunk_base[0];
     // the chunk's exclusive move offsets (each quarter's block scans the chunk)
     u64 tot64;
     sh.sexcl[tid] = (u32)block_excl_scan64<4>(cnt, sh.wsum, &tot64);
@@ -708,6 +710,31 @@ __global__ __launch_bounds__(256) void k_emit_desc(const Board* __restrict__ nod
       ++o;
     });
   }
+}
+
+// One slice [s0, s0 + len) of the grandparent level `lvl` (lo = 0) for the
+// sliced fused final stage: out[0] = its nodes {0, n}, out[1] = its children's
+// move words {0, w} (from the level's chunk offsets; words_total = the level's
+// child Range), the slice's group counter zeroed.  A slice past `cap` words is
+// flagged (overflow: exact rerun) and emptied.
+__global__ void k_wide_slice(const Range* __restrict__ lvl, const u64* __restrict__ chunk_base,
+                             const Range* __restrict__ words_total, u64 s0, u64 len, Range* __restrict__ out,
+                             u32* __restrict__ counter, PerftResult* __restrict__ res, u64 cap) {
+  const u64 n = lvl->hi - lvl->lo;
+  const u64 gn = s0 < n ? min(len, n - s0) : 0ull;
+  u64 w = 0;
+  if (gn) {
+    const u64 wbeg = chunk_base[s0 / kChunk];
+    const u64 wend = s0 + gn >= n ? words_total->hi - words_total->lo : chunk_base[(s0 + gn) / kChunk];
+    w = wend - wbeg;
+  }
+  if (w > cap) {
+    res->overflow = 1;
+    w = 0;
+  }
+  out[0] = Range{0, w ? gn : 0ull};
+  out[1] = Range{0, w};
+  *counter = 0;
 }
 
 __global__ void k_slice(Range* rng, u32 shard, u32 n_shards) {
@@ -1426,7 +1453,7 @@ template <int STM_G, u32 CAP, int MINW = 4, class W = u32>
 __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, const Range* __restrict__ rng_ch,
                                                  const W* __restrict__ mw, u64* __restrict__ divide,
-                                                 u32* __restrict__ next_group) {
+                                                 u32* __restrict__ next_group, ResultCursor* __restrict__ rcur) {
   __shared__ C2cShared<CAP> sh;
   tag_hist_init(sh.hist);
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1477,6 +1504,31 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
 #endif
   }
   tag_hist_flush(sh.hist, divide, otid(wave));
+  if (rcur) {
+    // dc_perft_repeat_device: the last block to finish stores the run's result
+    // at the cursor (k_copy_result's work, without its launch: ~5 us a step)
+    PerftResult* res = reinterpret_cast<PerftResult*>(divide);
+    __threadfence();  // this block's divide atomics before its done count
+    __syncthreads();
+    if (t0) sh.next = atomicAdd(&res->blocks_done, 1u);
+    __syncthreads();
+    if (sh.next == gridDim.x - 1) {  // block-uniform
+      __threadfence();
+      const ResultCursor rc = *rcur;  // every thread reads it before thread 0 advances it
+      u64* out = rc.base + 258 * rc.idx;
+      const u32 i = otid(wave), nr = res->n_root;
+      const u64 v = i < nr ? atomicAdd((unsigned long long*)&res->divide[i], 0ull) : 0ull;  // L2-coherent read
+      out[i] = v;
+      const u64 s = wave_sum64(v);
+      if (lane_id() == 0) sh.wsum[wave] = s;
+      __syncthreads();
+      if (t0) {
+        out[256] = (u64)nr | ((u64)res->overflow << 32);
+        out[257] = sh.wsum[0] + sh.wsum[1] + sh.wsum[2] + sh.wsum[3];
+        rcur->idx = rc.idx + 1;
+      }
+    }
+  }
 }
 
 // ------------------------------------------------- K4: per-lane DFS (REF)
@@ -1724,6 +1776,13 @@ hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, ResultCurs
   return hipGetLastError();
 }
 
+hipError_t launch_wide_slice(hipStream_t st, const Range* lvl, const u64* chunk_base, const Range* words_total,
+                             u64 s0, u64 len, Range* out, u32* counter, PerftResult* res, u64 cap) {
+  hipLaunchKernelGGL(k_wide_slice, dim3(1), dim3(1), 0, st, lvl, chunk_base, words_total, s0, len, out, counter, res,
+                     cap);
+  return hipGetLastError();
+}
+
 hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
   hipLaunchKernelGGL(k_slice, dim3(1), dim3(1), 0, st, rng, shard, n_shards);
   return hipGetLastError();
@@ -1871,25 +1930,26 @@ constexpr u32 kC3cCap = kC2cCap;
 #endif
 template <class W>
 static hipError_t count3c_w(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                            const Range* rng_ch, const W* mw, PerftResult* res) {
+                            const Range* rng_ch, const W* mw, PerftResult* res, ResultCursor* rcur, u32* counter) {
+  u32* next = counter ? counter : &res->next_chunk;
   if (stm_g) {
     auto k = k_count3c<1, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
-                       res->divide, &res->next_chunk);
+                       res->divide, next, rcur);
   } else {
     auto k = k_count3c<0, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
-                       res->divide, &res->next_chunk);
+                       res->divide, next, rcur);
   }
   return hipGetLastError();
 }
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u32* mw, PerftResult* res) {
-  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res);
+                          const Range* rng_ch, const u32* mw, PerftResult* res, ResultCursor* rcur, u32* counter) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, rcur, counter);
 }
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u64* mw, PerftResult* res) {
-  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res);
+                          const Range* rng_ch, const u64* mw, PerftResult* res, ResultCursor* rcur, u32* counter) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, rcur, counter);
 }
 
 // Product: REF -> k_count2c (the bulk split), FIDE -> k_count2b<FideRules>.

@@ -45,8 +45,8 @@ def d8_path(request, monkeypatch):
 
 @pytest.mark.parametrize("fen,depth", SPARSE, ids=[f"d{d}-{i}" for i, (_, d) in enumerate(SPARSE)])
 def test_dfs_sparse_vs_fastcpu(engine, fen, depth, d8_path):
-    if depth != 8 and d8_path == "fused":
-        pytest.skip("the path switch applies at depth 8 only")
+    if depth > 9 and d8_path == "fused":
+        pytest.skip("the path switch applies at depths 8 and 9 only")
     p = O.Pos.from_fen(fen)
     want, wdiv, wrm = O.fast_perft(p, depth, O.REF, threads=min(16, os.cpu_count() or 1))
     tot, div, rm = engine.perft(dchess.pos_from_fen(fen), depth)
@@ -107,14 +107,30 @@ def test_perft8_repeat_device(engine, d8_path):
     assert not (res[:, 256] >> np.uint64(32)).any()
 
 
-def test_perft9_startpos_golden(engine):
-    """perft(startpos, 9) through K4 at L = 2 (explicit per-lane stack of one
-    frame): total and divide against fastcpu's golden (2.6e12 leaves, 2.5 h on
-    8 host threads; ~0.6 s here).  The BFS levels stop at ply 5 (167 MB)."""
+def test_perft9_startpos_golden(engine, d8_path):
+    """perft(startpos, 9): total and divide against fastcpu's golden (2.6e12
+    leaves, 2.5 h on 8 host threads) through the sliced fused final stage
+    (ply 6 as boards, 4.3 GB; ply 7 as 64-bit words per slice of 2^21 ply-6
+    nodes) and through K4 at L = 2 (explicit per-lane stack of one frame, BFS
+    levels stopping at ply 5)."""
     g = DEEP["startpos_d9"]
     tot, div, rm = engine.perft(dchess.startpos(), 9)
     assert tot == g["total"] == 2_597_923_551_373
     assert {str(int(m)): int(v) for m, v in zip(rm, div)} == g["divide"]
+
+
+def test_perft9_wide_level_overflow_falls_back_to_k4(monkeypatch):
+    """Ply 6 larger than the sliced stage's level budget: the speculative run is
+    flagged, the exact rerun takes K4 from ply 5 (budget lowered through
+    DCHESS_PERFT_WIDE_LEVEL_MAX on a fresh context, sparse position)."""
+    monkeypatch.delenv("DCHESS_PERFT_K4", raising=False)
+    monkeypatch.setenv("DCHESS_PERFT_WIDE_LEVEL_MAX", "100000")
+    fen = SPARSE[2][0]
+    want, _, _ = O.fast_perft(O.Pos.from_fen(fen), 9, O.REF, threads=min(16, os.cpu_count() or 1))
+    eng = dchess.Engine(0)
+    eng.set_profiling(True)
+    assert eng.perft(dchess.pos_from_fen(fen), 9)[0] == want
+    assert eng.kernel_stats("dfs")["launches"] == 1
 
 
 def test_depth_beyond_k4_unsupported(engine):

@@ -19,7 +19,8 @@ bench.py turns these into fractions of the 78.6 T lane-op/s issue peak with the
 kernel's live HIP-event time.
 
 --units takes KEY=PATTERN=UNITS triples, e.g. final_d7=k_count2c<=3282734510:
-the first kernel whose name contains PATTERN is written under KEY.
+the first kernel whose name contains PATTERN (every '&'-separated part of it)
+is written under KEY.
 """
 import argparse
 import collections
@@ -79,7 +80,7 @@ if a.json:
     for spec in a.units:
         key, pat, units = spec.split("=")
         for k, c in avg.items():
-            if pat in k:
+            if all(part in k for part in pat.split("&")):
                 rec = {"kernel": k, "units_per_dispatch": float(units), "counters_per_dispatch": c,
                        "resources": meta[k], "source": a.source}
                 rec.update(derived(c, float(units)))
