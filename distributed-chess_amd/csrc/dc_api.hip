@@ -1126,13 +1126,8 @@ static bool fused3_enabled() {
 // copy.  *host_sync is set when a level size had to be read back on the host
 // (exact mode or a level beyond the speculative budget): such a sequence
 // depends on data and is never captured as a graph.
-// rcur (dc_perft_repeat_device): where the run's result goes; *copied is set
-// when the final stage stored it there itself (k_count3c's last block), else
-// the caller launches k_copy_result.
 int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
-                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true,
-                  dc::ResultCursor* rcur = nullptr, bool* copied = nullptr) {
-  if (copied) *copied = false;
+                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true) {
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
@@ -1290,7 +1285,6 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       c->last_final = "count2";
       for (u64 k = 0; k < n_slices; ++k) {
         const u64 s0 = k * kSliceNodes;
-        const bool last = k + 1 == n_slices;
         HIP_TRY(dc::launch_wide_slice(c->stream, c->rng.p + L, c->chunk_base.p, c->rng.p + L + 1, s0, kSliceNodes,
                                       c->slice_rng.p, c->slice_ctr.p, c->res.p, cap_w));
         HIP_TRY(c->timed("level_moves", 0, [&] {
@@ -1300,11 +1294,9 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
         }));
         HIP_TRY(c->timed("count2", 0, [&] {
           return dc::launch_count3c(c->stream, stm, c->nodes[buf].p + s0, c->tags[buf].p + s0, c->slice_rng.p,
-                                    c->slice_rng.p + 1, c->move_words64.p, c->res.p, last ? rcur : nullptr,
-                                    c->slice_ctr.p);
+                                    c->slice_rng.p + 1, c->move_words64.p, c->res.p, c->slice_ctr.p);
         }));
       }
-      if (copied) *copied = rcur != nullptr;
       return DC_SUCCESS;
     }
     if (fused3 && L + 1 == F && (!exact || wide || nb <= dc::kMoveWordNodesMax)) {
@@ -1338,11 +1330,10 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       c->last_final = "count2";
       HIP_TRY(c->timed("count2", 0, [&] {
         return wide ? dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L,
-                                         c->rng.p + L + 1, c->move_words64.p, c->res.p, rcur)
+                                         c->rng.p + L + 1, c->move_words64.p, c->res.p)
                     : dc::launch_count3c(c->stream, stm, c->nodes[buf].p, c->tags[buf].p, c->rng.p + L,
-                                         c->rng.p + L + 1, c->move_words.p, c->res.p, rcur);
+                                         c->rng.p + L + 1, c->move_words.p, c->res.p);
       }));
-      if (copied) *copied = rcur != nullptr;
       return DC_SUCCESS;
     }
     // Speculative mode never reads a level size back: the next level gets
@@ -1549,10 +1540,10 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
       // (one host sync per level), each result still left on the device
       HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out)));
       for (u32 i = 0; i < n_runs; ++i) {
-        bool hs = false, copied = false;
-        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs, true, c->rcur.p, &copied);
+        bool hs = false;
+        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs);
         if (e != DC_SUCCESS) return e;
-        if (!copied) HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
+        HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
       }
       return DC_SUCCESS;
     }
@@ -1563,12 +1554,10 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
         c->rgraph = nullptr;
       }
       if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-        bool hs = false, copied = false;
+        bool hs = false;
         // the result copy is part of the graph: its destination is the cursor
-        int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false, c->rcur.p,
-                               &copied);
-        if (ce == DC_SUCCESS && !copied && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess)
-          ce = DC_EHIP;
+        int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
+        if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
         hipGraph_t g = nullptr;
         const hipError_t ee = hipStreamEndCapture(c->stream, &g);
         if (ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
@@ -1598,11 +1587,10 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
     } else {
-      bool host_sync = false, copied = false;
-      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync, true, c->rcur.p,
-                            &copied);
+      bool host_sync = false;
+      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync);
       if (e != DC_SUCCESS) return e;
-      if (!copied) HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
+      HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
     }
   }
   return DC_SUCCESS;

@@ -19,7 +19,7 @@ struct PerftResult {
   u32 next_chunk;  // k_count2c's dynamic chunk counter (zeroed with the block)
   u64 level_n[16];
   u32 dfs_next;    // k_perft_dfs's frontier cursor (zeroed with the block)
-  u32 blocks_done; // k_count3c's finished blocks (the last one copies the result; zeroed with the block)
+  u32 pad0;
 };
 
 // Scratch of the single-workgroup top expansion (plies 1 and 2).
@@ -94,15 +94,13 @@ constexpr u64 kMoveWordNodesMax = 1ull << 20;
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
                               const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap);
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u32* mw, PerftResult* res, ResultCursor* rcur = nullptr,
-                          u32* counter = nullptr);
+                          const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter = nullptr);
 // The same with u64 words {grandparent index << 12 | f | t << 6} (no 2^20
 // grandparent limit): REF perft(8)'s final stage below ply 5.
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
                               const u32* counts, const u64* chunk_base, u64* mw, u64 mw_cap);
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u64* mw, PerftResult* res, ResultCursor* rcur = nullptr,
-                          u32* counter = nullptr);
+                          const Range* rng_ch, const u64* mw, PerftResult* res, u32* counter = nullptr);
 // The sliced fused final stage (REF perft(9)): slice [s0, s0 + len) of the
 // grandparent level `lvl` -> out[0] its node Range, out[1] its word Range,
 // *counter = 0 (k_count3c's group counter for the slice); a slice of more

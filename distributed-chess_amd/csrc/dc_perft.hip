@@ -1453,7 +1453,7 @@ template <int STM_G, u32 CAP, int MINW = 4, class W = u32>
 __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, const Range* __restrict__ rng_ch,
                                                  const W* __restrict__ mw, u64* __restrict__ divide,
-                                                 u32* __restrict__ next_group, ResultCursor* __restrict__ rcur) {
+                                                 u32* __restrict__ next_group) {
   __shared__ C2cShared<CAP> sh;
   tag_hist_init(sh.hist);
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1504,31 +1504,6 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
 #endif
   }
   tag_hist_flush(sh.hist, divide, otid(wave));
-  if (rcur) {
-    // dc_perft_repeat_device: the last block to finish stores the run's result
-    // at the cursor (k_copy_result's work, without its launch: ~5 us a step)
-    PerftResult* res = reinterpret_cast<PerftResult*>(divide);
-    __threadfence();  // this block's divide atomics before its done count
-    __syncthreads();
-    if (t0) sh.next = atomicAdd(&res->blocks_done, 1u);
-    __syncthreads();
-    if (sh.next == gridDim.x - 1) {  // block-uniform
-      __threadfence();
-      const ResultCursor rc = *rcur;  // every thread reads it before thread 0 advances it
-      u64* out = rc.base + 258 * rc.idx;
-      const u32 i = otid(wave), nr = res->n_root;
-      const u64 v = i < nr ? atomicAdd((unsigned long long*)&res->divide[i], 0ull) : 0ull;  // L2-coherent read
-      out[i] = v;
-      const u64 s = wave_sum64(v);
-      if (lane_id() == 0) sh.wsum[wave] = s;
-      __syncthreads();
-      if (t0) {
-        out[256] = (u64)nr | ((u64)res->overflow << 32);
-        out[257] = sh.wsum[0] + sh.wsum[1] + sh.wsum[2] + sh.wsum[3];
-        rcur->idx = rc.idx + 1;
-      }
-    }
-  }
 }
 
 // ------------------------------------------------- K4: per-lane DFS (REF)
@@ -1930,26 +1905,26 @@ constexpr u32 kC3cCap = kC2cCap;
 #endif
 template <class W>
 static hipError_t count3c_w(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                            const Range* rng_ch, const W* mw, PerftResult* res, ResultCursor* rcur, u32* counter) {
+                            const Range* rng_ch, const W* mw, PerftResult* res, u32* counter) {
   u32* next = counter ? counter : &res->next_chunk;
   if (stm_g) {
     auto k = k_count3c<1, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
-                       res->divide, next, rcur);
+                       res->divide, next);
   } else {
     auto k = k_count3c<0, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
-                       res->divide, next, rcur);
+                       res->divide, next);
   }
   return hipGetLastError();
 }
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u32* mw, PerftResult* res, ResultCursor* rcur, u32* counter) {
-  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, rcur, counter);
+                          const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, counter);
 }
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u64* mw, PerftResult* res, ResultCursor* rcur, u32* counter) {
-  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, rcur, counter);
+                          const Range* rng_ch, const u64* mw, PerftResult* res, u32* counter) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, counter);
 }
 
 // Product: REF -> k_count2c (the bulk split), FIDE -> k_count2b<FideRules>.
