@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 session m: the round-2 failing final stage (the whole round-2 tree,
 # commit 3d8df08, built with -DDC_C2C_SOA=1: k_count3c spills 48 B/lane) under
-# the ROCr scratch-management switches.  If a switch that changes how the
+# the ROCr scratch-management switches (tree: tools/build_r2tree.sh).  If a switch that changes how the
 # runtime grows, limits or reclaims scratch makes perft(6) exact, the fault
 # lies in scratch management, not in the kernel's code.  3 runs per setting.
 # CFGS="ROC_GLOBAL_CU_MASK=0x1 ..." runs the same under a CU mask (fewer CUs,
