@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -121,13 +122,24 @@ struct dc_ctx {
   u64* replay_host = nullptr;            // pinned: the replay kernel's five counters
   struct HostIo* host_io = nullptr;      // pinned: small validate / apply batches, read and written in place
   uint32_t io_seq = 0;                   // last completion flag value published into host_io->done
+  // dc_live_validator: the resident wave's mailbox (pinned, coherent), its
+  // stream, the requests it has served and its lease (0: off)
+  dc::LiveBox* live = nullptr;
+  hipStream_t live_stream = nullptr;
+  uint32_t live_seq = 0;
+  uint32_t live_lease_us = 0;
+  bool live_running = false;
   // The last perft launch sequence, captured as a hipGraph (see perft_run).
   struct PerftKey {
     u32 rules, depth, split, shard, n_shards, stm, k4;
     uint64_t epoch;
+    // the capacities a captured graph was sized with (test knobs
+    // DCHESS_PERFT_WIDE_MAX / _WIDE_LEVEL_MAX): a changed knob re-captures
+    uint64_t wide_words, wide_level;
     bool operator==(const PerftKey& o) const {
       return rules == o.rules && depth == o.depth && split == o.split && shard == o.shard &&
-             n_shards == o.n_shards && stm == o.stm && k4 == o.k4 && epoch == o.epoch;
+             n_shards == o.n_shards && stm == o.stm && k4 == o.k4 && epoch == o.epoch &&
+             wide_words == o.wide_words && wide_level == o.wide_level;
     }
   } pkey{};
   hipGraphExec_t pgraph = nullptr;
@@ -200,6 +212,8 @@ struct dc_ctx {
     if (res_host) (void)hipHostFree(res_host);
     if (replay_host) (void)hipHostFree(replay_host);
     if (host_io) (void)hipHostFree(host_io);
+    if (live) (void)hipHostFree(live);
+    if (live_stream) (void)hipStreamDestroy(live_stream);
     if (root_host) (void)hipHostFree(root_host);
     pos.release();
     verdicts.release();
@@ -365,9 +379,12 @@ int dc_ctx_create(int device, dc_ctx** out) {
   return DC_SUCCESS;
 }
 
+static int live_stop(dc_ctx* c);
+
 int dc_ctx_destroy(dc_ctx* c) {
   if (!c) return DC_EINVAL;
   (void)hipSetDevice(c->device);
+  (void)live_stop(c);
   (void)hipStreamSynchronize(c->stream);
   delete c;
   return DC_SUCCESS;
@@ -549,12 +566,126 @@ int dc_move_pack_batch(const uint32_t* actions, uint32_t n, uint16_t* moves) {
   return DC_SUCCESS;
 }
 
+// ========================================================= live validator
+// dc_live_validator(ctx, lease_us): small validate / apply calls (n <= 64,
+// not profiling) go to one resident wave (k_live, dc_moves.hip) through the
+// stamped mailbox of dc_kernels.h instead of a kernel launch each.  The wave
+// leaves after lease_us without a request (and on dc_live_validator(ctx, 0) or
+// dc_ctx_destroy); the next call starts it again.  While it runs, a
+// device-wide synchronisation (hipDeviceSynchronize) waits for its lease.
+static int live_stop(dc_ctx* c) {
+  if (!c->live_running) return DC_SUCCESS;
+  __atomic_store_n(&c->live->ctl, 1u, __ATOMIC_RELEASE);
+  const hipError_t e = hipStreamSynchronize(c->live_stream);
+  __atomic_store_n(&c->live->ctl, 0u, __ATOMIC_RELEASE);
+  c->live_running = false;
+  return e == hipSuccess ? DC_SUCCESS : DC_EHIP;
+}
+
+static int live_start(dc_ctx* c) {
+  __atomic_store_n(&c->live->state, 0u, __ATOMIC_RELEASE);
+  __atomic_store_n(&c->live->ctl, 0u, __ATOMIC_RELEASE);
+  HIP_TRY(dc::launch_live(c->live_stream, c->live, c->live_seq, (u64)c->live_lease_us * 100));  // 100 MHz clock
+  c->live_running = true;
+  return DC_SUCCESS;
+}
+
+int dc_live_validator(dc_ctx* c, uint32_t lease_us) {
+  ENTER(c);
+  if (lease_us == 0) {
+    const int e = live_stop(c);
+    c->live_lease_us = 0;
+    return e;
+  }
+  if (lease_us > 60u * 1000 * 1000) return DC_EINVAL;  // at most a minute
+  if (!c->live) {
+    HIP_TRY(hipHostMalloc((void**)&c->live, sizeof(dc::LiveBox), hipHostMallocCoherent));
+    std::memset((void*)c->live, 0, sizeof(dc::LiveBox));
+  }
+  if (!c->live_stream) HIP_TRY(hipStreamCreateWithFlags(&c->live_stream, hipStreamNonBlocking));
+  if (c->live_running && lease_us != c->live_lease_us) {
+    const int e = live_stop(c);  // the running wave holds the old lease
+    if (e != DC_SUCCESS) return e;
+  }
+  c->live_lease_us = lease_us;
+  return DC_SUCCESS;
+}
+
+// One request through the mailbox.  pos_out (apply) may alias pos.
+static int live_call(dc_ctx* c, bool apply, bool fide, const dc_pos* pos, const uint16_t* moves, uint32_t n,
+                     uint8_t* verdicts, uint8_t* info, dc_pos* pos_out) {
+  dc::LiveBox* b = c->live;
+  if (!c->live_running) {
+    const int e = live_start(c);
+    if (e != DC_SUCCESS) return e;
+  }
+  const uint32_t seq = c->live_seq + 1;
+  const uint32_t st = dc::live_stamp(seq) << 16;
+  if (seq % dc::kLiveClearEvery == 0) std::memset((void*)b->req, 0, sizeof(b->req));
+  const uint32_t nw = apply ? dc::kLiveFields * n : n;  // response words read back
+  for (uint32_t i = 0; i < nw; ++i) __atomic_store_n(&b->resp[i], 0u, __ATOMIC_RELAXED);
+  for (uint32_t e = 0; e < n; ++e) {
+    uint16_t h[dc::kLiveFields];
+    std::memcpy(h, pos[e].bb, 32);
+    h[16] = (uint16_t)(pos[e].stm | (pos[e].castle << 8));
+    h[17] = (uint8_t)pos[e].ep;
+    h[18] = moves[e];
+    for (uint32_t k = 0; k < dc::kLiveFields; ++k) b->req[1 + k * n + e] = st | h[k];
+  }
+  __atomic_store_n(&b->req[0], st | n | ((uint32_t)apply << 7) | ((uint32_t)fide << 8), __ATOMIC_RELEASE);
+  // spin on the response words; a wave that stopped (lease) before taking the
+  // request is restarted -- it takes requests only before it publishes state 2
+  auto complete = [&]() {
+    for (uint32_t i = 0; i < nw; ++i)
+      if ((__atomic_load_n(&b->resp[i], __ATOMIC_ACQUIRE) & 0xFFFF0000u) != st) return false;
+    return true;
+  };
+  u64 spins = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!complete()) {
+    if ((++spins & 255) == 0) {
+      if (__atomic_load_n(&b->state, __ATOMIC_ACQUIRE) == 2u) {
+        HIP_TRY(hipStreamSynchronize(c->live_stream));
+        c->live_running = false;
+        if (complete()) break;
+        const int e = live_start(c);
+        if (e != DC_SUCCESS) return e;
+      } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+        (void)live_stop(c);
+        return DC_EHIP;  // the wave neither answered nor stopped
+      }
+    }
+  }
+  c->live_seq = seq;
+  for (uint32_t e = 0; e < n; ++e) {
+    const uint32_t w = b->resp[e];
+    verdicts[e] = (uint8_t)(w & 0xFF);
+    if (info) info[e] = (uint8_t)((w >> 8) & 0xFF);
+    if (apply) {
+      uint16_t h[dc::kLiveFields];
+      for (uint32_t k = 1; k < dc::kLiveFields; ++k) h[k] = (uint16_t)b->resp[k * n + e];
+      dc_pos q = pos[e];
+      std::memcpy(q.bb, h + 1, 32);
+      q.stm = (uint8_t)(h[17] & 0xFF);
+      q.castle = (uint8_t)(h[17] >> 8);
+      q.ep = (int8_t)(uint8_t)h[18];
+      pos_out[e] = q;
+    }
+  }
+  return DC_SUCCESS;
+}
+
+static bool live_eligible(const dc_ctx* c, uint32_t n) {
+  return c->live_lease_us && n <= dc::kLiveMax && !c->profiling;
+}
+
 // ============================================================== validation
 int dc_validate_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, const uint16_t* moves, uint32_t n,
                       uint8_t* verdicts) {
   ENTER(c);
   if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
   if (n == 0) return DC_SUCCESS;
+  if (live_eligible(c, n)) return live_call(c, false, rules == DC_RULES_FIDE, pos, moves, n, verdicts, nullptr, nullptr);
   if (n <= kHostIoBatch) {  // pinned, read in place by the kernel
     if (!c->host_io) {
       HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo), hipHostMallocCoherent));
@@ -594,6 +725,7 @@ int dc_apply_batch(dc_ctx* c, uint32_t rules, dc_pos* pos, const uint16_t* moves
   ENTER(c);
   if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
   if (n == 0) return DC_SUCCESS;
+  if (live_eligible(c, n)) return live_call(c, true, rules == DC_RULES_FIDE, pos, moves, n, verdicts, info, pos);
   if (n <= kHostIoBatch) {  // pinned, read and written in place by the kernel
     if (!c->host_io) {
       HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo), hipHostMallocCoherent));
@@ -723,6 +855,9 @@ int dc_replay_info(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_
   if (rules > DC_RULES_FIDE || (n_games && n_plies && (!moves || !info))) return DC_EINVAL;
   if (rules != DC_RULES_REF) return DC_EUNSUPPORTED;
   const size_t nm = (size_t)n_games * n_plies;
+  // replay_impl's limit (n_games * n_plies * 2 < 4 GiB), checked before any
+  // buffer is sized or any byte is copied
+  if (nm * 2 >= (1ull << 32)) return DC_EUNSUPPORTED;
   const size_t words = (size_t)((n_games + 63) / 64) * n_plies;
   HIP_TRY(c->moves.ensure(std::max<size_t>(nm, 1)));
   HIP_TRY(c->replay_info.ensure(std::max<size_t>(nm, 1)));
@@ -1132,7 +1267,13 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   const bool sharded = n_shards > 1;
   u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
   // REF perft(8) and (9): 64-bit move words below ply 5 or slices of ply 6 (see kWideWordsMax)
-  const bool wide = !fide && (depth == kDfsFrontier + 3 || depth == kDfsFrontier + 4) && !perft_k4_forced();
+  // (the sliced stage indexes its grandparent level from 0: a contiguous shard
+  // cut at that very level (DC_SHARD=contig, A/B build) starts elsewhere, so
+  // that combination takes K4 instead)
+  const bool contig_at_sliced = shard_contiguous() && sharded && depth == kDfsFrontier + 4 &&
+                                std::max<u32>(1, std::min(split_depth, depth - 2)) == depth - 3;
+  const bool wide = !fide && (depth == kDfsFrontier + 3 || depth == kDfsFrontier + 4) && !perft_k4_forced() &&
+                    !contig_at_sliced;
   const bool sliced = wide && depth == kDfsFrontier + 4;
   // REF beyond ply kDfsFrontier: K4 walks the last Ldfs plies above the final
   // stage per lane (k_perft_dfs) instead of materialising those levels
@@ -1418,7 +1559,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
               uint32_t n_shards, bool exact, dc::PerftResult* out) {
   const bool graphable = !exact && !c->profiling && perft_graphs_enabled();
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
-                       g_alloc_epoch.load()};
+                       g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
   if (graphable && c->pgraph && c->pkey == key) {
     int e = write_root_host(c, pos);
     if (e != DC_SUCCESS) return e;
@@ -1527,7 +1668,7 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
   if (n_runs == 0) return DC_SUCCESS;
   HIP_TRY(c->rcur.ensure(1));  // before the key: an allocation moves the epoch
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
-                       g_alloc_epoch.load()};
+                       g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
   const bool graphable = !c->profiling && perft_graphs_enabled();
   if (!c->root_host || !(graphable && c->rgraph && c->rkey == key)) {
     // a plain run (host sync) sizes the buffers and stages the root; then the

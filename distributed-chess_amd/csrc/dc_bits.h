@@ -31,10 +31,12 @@ constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
 // so one 64-bit shift (4 cycles per wave) beats the compiler's habit of
 // splitting it into v_alignbit_b32 + v_lshlrev_b32 once the halves feed
 // 32-bit bitop3s (tools/ubench/vop_rate.hip, profiles/r01/ubench_vop.txt).
-// DC_SHIFT_PAD (A/B diagnostics only): 1 = s_nop 1 ahead of the shift inside
-// the statement, 2 = s_nop 1 after it, 3 = plain C shifts (no asm).
+// DC_SHIFT_PAD selects how the shift is written: 4 (shipped since round 4)
+// an opaque SGPR shift amount, see shift_amount; 0 the round-1..3 inline-asm
+// shift; A/B diagnostics only: 1 = s_nop 1 ahead of the asm shift, 2 = s_nop 1
+// after it, 3 = plain C shifts.
 #ifndef DC_SHIFT_PAD
-#define DC_SHIFT_PAD 0
+#define DC_SHIFT_PAD 4
 #endif
 #if DC_SHIFT_PAD == 1
 #define DC_SHL_ASM "s_nop 1\n\tv_lshlrev_b64 %0, %1, %2"
@@ -46,10 +48,27 @@ constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
 #define DC_SHL_ASM "v_lshlrev_b64 %0, %1, %2"
 #define DC_SHR_ASM "v_lshrrev_b64 %0, %1, %2"
 #endif
+// The shift amount as an opaque SGPR constant (DC_SHIFT_PAD == 4, round 4):
+// the compiler cannot split a shift by an unknown amount into 32-bit halves,
+// so it emits the one v_lshlrev_b64 itself -- and, unlike after an inline-asm
+// shift, it knows that instruction's hazards, so no conservative s_nop 0
+// follows each shift (15M s_nop per perft(7) launch of k_count3c,
+// tools/bbprof.py).
+template <int A>
+__device__ __forceinline__ u32 shift_amount() {
+  u32 k;
+  asm("s_mov_b32 %0, %1" : "=s"(k) : "i"(A));
+  return k;
+}
 template <int S>
 __device__ __forceinline__ u64 sh(u64 x) {
   u64 r;
-#if DC_SHIFT_PAD == 3
+#if DC_SHIFT_PAD == 4
+  if constexpr (S >= 32) r = (u64)((u32)x << (S - 32)) << 32;
+  else if constexpr (S <= -32) r = (u64)((u32)(x >> 32) >> (-S - 32));
+  else if constexpr (S > 0) r = x << shift_amount<S>();
+  else if constexpr (S < 0) r = x >> shift_amount<-S>();
+#elif DC_SHIFT_PAD == 3
   if constexpr (S > 0) r = x << S;
   else if constexpr (S < 0) r = x >> -S;
 #else

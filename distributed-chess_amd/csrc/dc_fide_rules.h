@@ -117,32 +117,24 @@ struct Analysis {
   int ksq;       // our king square, -1 if none
 };
 
-// First occupied square along direction D from s inside `ray`.
-template <bool UP>
-__device__ __forceinline__ int first_on(u64 x) {
-  if constexpr (UP) return lsb(x);
-  else return msb(x);
-}
-
+// Branch-free on purpose: with `checkers |= m1; return;` on one path and
+// `pinned |= m1` on another, the compiler merged the two stores into one
+// store through a selected address (&a.checkers or &a.pinned), which kept the
+// whole Analysis in scratch memory (round 3: 536 B/lane in k_count2b<Fide>).
+// Two unconditional value updates keep both in registers.
 template <int STM, int D>
-__device__ __forceinline__ void scan_dir(const FPos<STM>& f, int ksq, const Lines& l, Analysis& a) {
+__device__ __forceinline__ void scan_dir(const FPos<STM>& f, int ksq, const Lines& l, u64& checkers, u64& pinned) {
   constexpr bool UP = (D & 1) == 0;  // 0 N, 2 E, 4 NE, 6 NW go to higher squares
   const u64 line = (D < 2) ? l.file : (D < 4) ? l.rank : (D < 6) ? l.diag : l.anti;
   const u64 ray = line & (UP ? above_mask(ksq) : below_mask(ksq));
   const u64 sl = (D < 4) ? f.tO : f.tD;
   const u64 blk = f.occ & ray;
-  if (!blk) return;
-  const int b1 = first_on<UP>(blk);
-  const u64 m1 = 1ull << b1;
-  if (m1 & sl) {
-    a.checkers |= m1;
-    return;
-  }
-  if (!(m1 & f.us)) return;
+  // first and second occupied squares on the ray (bits; 0 when absent)
+  const u64 m1 = UP ? (blk & (0ull - blk)) : (blk ? (1ull << msb(blk)) : 0ull);
   const u64 rest = blk & ~m1;
-  if (!rest) return;
-  const int b2 = first_on<UP>(rest);
-  if ((1ull << b2) & sl) a.pinned |= m1;
+  const u64 m2 = UP ? (rest & (0ull - rest)) : (rest ? (1ull << msb(rest)) : 0ull);
+  checkers |= m1 & sl;
+  pinned |= ((m2 & sl) ? (m1 & f.us) : 0ull);
 }
 
 template <int STM>
@@ -159,15 +151,18 @@ __device__ __forceinline__ Analysis analyse(const FPos<STM>& f) {
   if (a.ksq < 0) return a;
   a.checkers = (pawn_attacks<STM>(f.K) & f.tP) | (knight_attacks(f.K) & f.tN);
   const Lines l = lines_of(a.ksq);
-  scan_dir<STM, 0>(f, a.ksq, l, a);
-  scan_dir<STM, 1>(f, a.ksq, l, a);
-  scan_dir<STM, 2>(f, a.ksq, l, a);
-  scan_dir<STM, 3>(f, a.ksq, l, a);
-  scan_dir<STM, 4>(f, a.ksq, l, a);
-  scan_dir<STM, 5>(f, a.ksq, l, a);
-  scan_dir<STM, 6>(f, a.ksq, l, a);
-  scan_dir<STM, 7>(f, a.ksq, l, a);
-  if (a.checkers) a.cmask = a.checkers | between(a.ksq, lsb(a.checkers));
+  u64 chk = a.checkers, pin = 0;
+  scan_dir<STM, 0>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 1>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 2>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 3>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 4>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 5>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 6>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 7>(f, a.ksq, l, chk, pin);
+  a.checkers = chk;
+  a.pinned = pin;
+  if (chk) a.cmask = chk | between(a.ksq, lsb(chk));
   return a;
 }
 

@@ -22,6 +22,34 @@ inline const char* ab_env(const char* name) {
 typedef unsigned long long u64;
 typedef uint32_t u32;
 
+}  // namespace dc
+
+// Basic-block execution counts (tools/bbprof.py, measurement builds only:
+// -DDC_BBPROF).  The counter array is written only by instrumentation that
+// tools/bbprof.py inserts into one kernel's assembly; the product never
+// defines DC_BBPROF.
+#ifdef DC_BBPROF
+#define DC_BBPROF_DEFINE(NAME)                                                                            \
+  __device__ unsigned long long dc_bbprof_##NAME[8192];                                                 \
+  extern "C" __attribute__((visibility("default"))) int dc_ab_bbprof_##NAME(unsigned long long* out,    \
+                                                                           int reset) {                 \
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(dc_bbprof_##NAME), sizeof(dc_bbprof_##NAME), 0,       \
+                                   hipMemcpyDeviceToHost) != hipSuccess)                                  \
+      return -1;                                                                                          \
+    if (reset) {                                                                                          \
+      static unsigned long long zero[8192];                                                               \
+      if (hipMemcpyToSymbol(HIP_SYMBOL(dc_bbprof_##NAME), zero, sizeof(zero), 0, hipMemcpyHostToDevice) !=  \
+          hipSuccess)                                                                                     \
+        return -1;                                                                                        \
+    }                                                                                                     \
+    return 0;                                                                                             \
+  }
+#else
+#define DC_BBPROF_DEFINE(NAME)
+#endif
+
+namespace dc {
+
 // One position: quad-bitboard of include/dchess.h (b0 black, b1..b3 kind bits).
 struct Board {
   u64 b0, b1, b2, b3;
@@ -52,6 +80,33 @@ __host__ __device__ inline void startpos_board(B& b) {
 }
 
 hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out, u32* done = nullptr, u32 seq = 0);
+
+// ---- the live validator (dc_live_validator): one resident wave that serves
+// small validate / apply calls from a pinned, coherent mailbox, so the live
+// n = 1 call of a voting replica costs a host store and a poll, not a launch.
+// Every mailbox dword is stamp << 16 | payload: a dword is written and read
+// whole, so a reader accepts a request (or a response) only when every dword
+// it needs carries the current stamp -- no fence orders one against another.
+// Stamps run 1..65535 (stamp(seq) = seq % 65535 + 1); the host zeroes the
+// request area every kLiveClearEvery requests and the response words before
+// each request, so a stale dword never carries the current stamp.
+// Request: word 0 = stamp | n (1..64) | apply << 7 | fide << 8; then
+// kLiveFields fields field-major (word 1 + k * n + e): 16 bitboard half-words,
+// stm | castle << 8, (u8)ep, the move.  Response: word k * n + e; k = 0 the
+// verdict | info << 8, k = 1..18 (apply) the position's fields.
+constexpr u32 kLiveMax = 64, kLiveFields = 19;
+constexpr u32 kLiveReqWords = 1 + kLiveFields * kLiveMax;
+constexpr u32 kLiveClearEvery = 16384;
+struct alignas(64) LiveBox {
+  u32 req[kLiveReqWords];
+  alignas(64) u32 resp[kLiveFields * kLiveMax];
+  alignas(64) u32 state;  // device -> host: 2 once the wave takes no more requests
+  alignas(64) u32 ctl;    // host -> device: 1 asks the wave to stop
+};
+__host__ __device__ inline u32 live_stamp(u32 seq) { return seq % 65535u + 1u; }
+// lease_ticks: the wave stops after that many wall-clock ticks (100 MHz) with
+// no request; `seq` = requests already served (the first one it takes is seq + 1)
+hipError_t launch_live(hipStream_t st, LiveBox* box, u32 seq, u64 lease_ticks);
 hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, u32 n, uint8_t* verdicts,
                             uint8_t* info, u32* done = nullptr, u32 seq = 0);
 // stats[5] = validated, accepted, rejected, digest sum, digest xor; partial has

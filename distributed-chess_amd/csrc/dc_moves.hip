@@ -10,6 +10,8 @@
 
 #include "dc_common.h"
 
+DC_BBPROF_DEFINE(moves)  // measurement builds only (tools/bbprof.py)
+
 namespace dc {
 
 // ------------------------------------------------------------- validation
@@ -1047,6 +1049,88 @@ __global__ __launch_bounds__(256) void k_gen_games_fide(u64 seed, u64 first_game
 }
 
 // ------------------------------------------------------------- launchers
+
+// ------------------------------------------------------- the live validator
+// One wave resident on one CU, launched on its own stream (dc_api.hip): polls
+// the request words of a pinned coherent LiveBox (dc_kernels.h) with
+// system-scope loads, validates (and applies) up to 64 moves, one per lane,
+// with the same per-move code as k_validate_ref / k_apply_ref (FIDE:
+// k_validate_fide / k_apply_fide), and writes stamped response words.  It
+// leaves when asked (ctl) or after lease_ticks without a request, always:
+// every loop trip reads the clock, so the wave cannot outlive its lease even
+// if the host never asks it to stop.
+__device__ __forceinline__ u32 sys_load(const u32* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(u32* p, u32 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ __launch_bounds__(64) void k_live(LiveBox* box, u32 seq, u64 lease_ticks) {
+  __shared__ uint16_t fld[kLiveFields * kLiveMax];
+  const u32 lane = threadIdx.x;
+  u64 t_last = wall_clock64();
+  for (;;) {
+    const u32 stamp = live_stamp(seq + 1);
+    const u32 w0 = sys_load(&box->req[lane]);
+    const u32 ctl = sys_load(&box->ctl);
+    const u32 hdr = lane_bcast(w0, 0);
+    if ((hdr >> 16) == stamp) {
+      const u32 n = min(max(hdr & 127u, 1u), kLiveMax);
+      const bool apply = (hdr >> 7) & 1, fide = (hdr >> 8) & 1;
+      const u32 words = 1 + kLiveFields * n;
+      bool torn = false;
+      for (u32 base = 0; base < words; base += 64) {
+        const u32 j = base + lane;
+        const u32 w = base == 0 ? w0 : (j < words ? sys_load(&box->req[j]) : 0u);
+        if (j < words) {
+          torn |= (w >> 16) != stamp;
+          if (j >= 1) fld[j - 1] = (uint16_t)w;
+        }
+      }
+      if (__ballot(torn)) continue;  // a request still being written: poll again
+      __syncthreads();
+      if (lane < n) {
+        auto f = [&](u32 k) -> u32 { return fld[k * n + lane]; };
+        DevPos p;
+        for (int q = 0; q < 4; ++q)
+          p.bb[q] = (u64)f(4 * q) | ((u64)f(4 * q + 1) << 16) | ((u64)f(4 * q + 2) << 32) | ((u64)f(4 * q + 3) << 48);
+        p.stm = (uint8_t)(f(16) & 0xFF);
+        p.castle = (uint8_t)(f(16) >> 8);
+        p.ep = (int8_t)(uint8_t)f(17);
+        p.r0 = 0;
+        p.r1 = 0;
+        const uint16_t mv = (uint16_t)f(18);
+        uint8_t v = 0, info = 0;
+        if (apply) {
+          if (fide) apply_fide_one(&p, &mv, 0, &v, &info);
+          else apply_ref_one(&p, &mv, 0, &v, &info);
+          const u32 sh = stamp << 16;
+          for (int q = 0; q < 4; ++q)
+            for (int h = 0; h < 4; ++h)
+              sys_store(&box->resp[(1 + 4 * q + h) * n + lane], sh | (u32)((p.bb[q] >> (16 * h)) & 0xFFFF));
+          sys_store(&box->resp[17 * n + lane], sh | p.stm | ((u32)p.castle << 8));
+          sys_store(&box->resp[18 * n + lane], sh | (u32)(uint8_t)p.ep);
+        } else {
+          const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+          v = (uint8_t)(fide ? fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), mv) : ref_verdict(b, p.stm & 1, mv));
+        }
+        sys_store(&box->resp[lane], (stamp << 16) | v | ((u32)info << 8));
+      }
+      __syncthreads();  // fld is rewritten by the next request
+      ++seq;
+      t_last = wall_clock64();
+      continue;
+    }
+    if (ctl == 1 || wall_clock64() - t_last > lease_ticks) break;
+  }
+  if (lane == 0) __hip_atomic_store(&box->state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_live(hipStream_t st, LiveBox* box, u32 seq, u64 lease_ticks) {
+  hipLaunchKernelGGL(k_live, dim3(1), dim3(64), 0, st, box, seq, lease_ticks);
+  return hipGetLastError();
+}
 
 hipError_t launch_validate_ref(hipStream_t st, const DevPos* pos, const uint16_t* moves, u32 n, uint8_t* out, u32* done,
                                u32 seq) {

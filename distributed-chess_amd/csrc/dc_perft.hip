@@ -32,11 +32,16 @@
 #include "dc_common.h"
 #include "dc_perft.h"
 
+DC_BBPROF_DEFINE(perft)  // measurement builds only (tools/bbprof.py)
+
 namespace dc {
 
 // ------------------------------------------------------------ rules policies
 struct RefRules {
   static constexpr bool kMeta = false;
+  // blocks of 256 per CU the level / final-stage kernels are built for
+  // (FIDE's legal-move analysis needs the registers of 2: spill-free)
+  static constexpr int kMinBlocks = 4;
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32) { return ref_count<STM>(b); }
   template <int STM, class V>
@@ -50,8 +55,12 @@ struct RefRules {
   }
 };
 
+#ifndef DC_FIDE_MINB
+#define DC_FIDE_MINB 2  // (A/B: 4 = the round-3 budget, 128 VGPRs with spills)
+#endif
 struct FideRules {
   static constexpr bool kMeta = true;
+  static constexpr int kMinBlocks = DC_FIDE_MINB;
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32 meta) { return fide_count<STM>(b, meta); }
   template <int STM, class V>
@@ -508,7 +517,7 @@ struct WriteShared {
 };
 
 template <class R, int STM>
-__global__ __launch_bounds__(256, 4) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+__global__ __launch_bounds__(256, R::kMinBlocks) void k_level_write(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                         const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                         const u32* __restrict__ counts, const u64* __restrict__ chunk_base,
                                                         Board* __restrict__ out, uint16_t* __restrict__ out_meta,
@@ -879,7 +888,7 @@ struct C2bShared {
 };
 
 template <class R, int STM>
-__global__ __launch_bounds__(256, 4) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+__global__ __launch_bounds__(256, R::kMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                     u64* __restrict__ divide) {
   __shared__ C2bShared sh;

@@ -80,6 +80,7 @@ def lib():
         "dc_move_pack_batch": (C.c_int, [_vp, C.c_uint32, _vp]),
         "dc_validate_batch": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, _vp]),
         "dc_apply_batch": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, _vp, _vp]),
+        "dc_live_validator": (C.c_int, [_vp, C.c_uint32]),
         "dc_replay": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp, C.POINTER(_Stats)]),
         "dc_replay_device": (C.c_int, [_vp, C.c_uint32, _vp, _vp, C.c_uint32, C.c_uint32, _vp, _vp,
                                        C.POINTER(_Stats)]),
@@ -352,6 +353,11 @@ class Engine:
         return DeviceBuffer(self, nbytes)
 
     # ---------------------------------------------------------- validation
+    def live_validator(self, lease_us):
+        """dc_live_validator: calls of <= 64 moves on this engine are served by
+        a resident wave (no launch per call) while the lease lasts; 0 stops it."""
+        _check(lib().dc_live_validator(self.ctx, int(lease_us)), "dc_live_validator")
+
     def validate_batch(self, pos, moves, rules=RULES_REF):
         pos = np.ascontiguousarray(pos, POS_DTYPE)
         moves = np.ascontiguousarray(moves, np.uint16)

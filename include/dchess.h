@@ -166,6 +166,18 @@ int dc_validate_batch(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, const uint
 int dc_apply_batch(dc_ctx* ctx, uint32_t rules, dc_pos* pos, const uint16_t* moves, uint32_t n,
                    uint8_t* verdicts, uint8_t* info);
 
+/* The live validator (opt-in, per context): with lease_us > 0, every
+ * dc_validate_batch / dc_apply_batch call of at most 64 moves on this context
+ * is served by one resident GPU wave that polls a pinned mailbox (no kernel
+ * launch per call) -- the n = 1 call is_valid_tx makes before a replica signs
+ * its vote (core/src/consensus/hotstuff.rs:138, :52).  Results are identical
+ * to the launched path.  The wave leaves after lease_us microseconds without a
+ * call (at most 60 s; the next call restarts it), on dc_live_validator(ctx, 0)
+ * and in dc_ctx_destroy.  While it is resident, a device-wide synchronisation
+ * (hipDeviceSynchronize) of the same process waits for the lease to run out:
+ * switch it off before one. */
+int dc_live_validator(dc_ctx* ctx, uint32_t lease_us);
+
 /* ------------------------------------------------------------------ replay
  * Replays n_games games of n_plies ply-major moves (moves[ply*n_games + g])
  * from *start (NULL = startpos).  Per ply: verdict; apply only if accepted

@@ -99,6 +99,7 @@ pub mod sys {
                                  verdicts: *mut u8) -> c_int;
         pub fn dc_apply_batch(ctx: *mut dc_ctx, rules: u32, pos: *mut dc_pos, moves: *const u16, n: u32,
                               verdicts: *mut u8, info: *mut u8) -> c_int;
+        pub fn dc_live_validator(ctx: *mut dc_ctx, lease_us: u32) -> c_int;
         // replay
         pub fn dc_replay(ctx: *mut dc_ctx, rules: u32, start: *const dc_pos, moves: *const u16, n_games: u32,
                          n_plies: u32, bitmap: *mut u64, digests: *mut u64, stats: *mut dc_replay_stats) -> c_int;
@@ -219,6 +220,12 @@ impl Engine {
         self.0
     }
 
+    /// Opt-in resident validator for this context (dc_live_validator): calls of
+    /// at most 64 moves skip the kernel launch while the lease lasts; 0 stops it.
+    pub fn live_validator(&self, lease_us: u32) -> Result<(), DcError> {
+        check(unsafe { sys::dc_live_validator(self.0, lease_us) }, "dc_live_validator")
+    }
+
     /// validate_move (chess.rs:82) for one (from, to) pair: n = 1, the live consensus call.
     pub fn validate(&self, pos: &sys::dc_pos, from: (u32, u32), to: (u32, u32)) -> Result<Verdict, DcError> {
         let mv = unsafe { sys::dc_move_pack(from.0, from.1, to.0, to.1) };
@@ -265,10 +272,13 @@ impl Engine {
     /// Resync: replay a game's committed moves in one call; returns the per-ply
     /// info bytes (0xFF = rejected) and the counters.
     pub fn replay_info(&self, moves: &[u16]) -> Result<(Vec<u8>, sys::dc_replay_stats), DcError> {
+        // n_plies is a u32 at the ABI: a longer log is an error, never truncated
+        let n_plies = u32::try_from(moves.len()).map_err(|_| DcError {
+            status: sys::DC_EINVAL, what: "dc_replay_info", text: "move log longer than u32::MAX plies".into() })?;
         let mut info = vec![0u8; moves.len()];
         let mut st = sys::dc_replay_stats::default();
         check(unsafe { sys::dc_replay_info(self.0, sys::DC_RULES_REF, std::ptr::null(), moves.as_ptr(), 1,
-                                           moves.len() as u32, std::ptr::null_mut(), std::ptr::null_mut(),
+                                           n_plies, std::ptr::null_mut(), std::ptr::null_mut(),
                                            info.as_mut_ptr(), &mut st) }, "dc_replay_info")?;
         Ok((info, st))
     }

@@ -8,6 +8,11 @@
 //   fe_mul A B | fe_sqr A | fe_add A B | fe_sub A B | fe_inv A | fe_sqrt A
 //   sc_mul A B | sc_inv A | mulg K | mulq K QX QY | hash W B FX FY TX TY
 //   tx W B FX FY TX TY SIG PK TURN
+//   timed R   then tx lines, then "end": the G table is built first, then the
+//             parsed transactions are checked R times under a steady_clock;
+//             prints the verdicts of one pass and "ns <elapsed of all passes>"
+//             (bench.py's cpu_baseline of the signature leg)
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <iostream>
@@ -45,6 +50,57 @@ static std::vector<Ge>& gtab() {
   return t;
 }
 
+struct TxIn {
+  std::string w, b, sig, pk;
+  u32 act[4];
+  int turn;
+};
+
+static TxIn parse_tx(std::istringstream& in) {
+  TxIn t;
+  t.turn = -1;
+  in >> t.w >> t.b >> t.act[0] >> t.act[1] >> t.act[2] >> t.act[3] >> t.sig >> t.pk >> t.turn;
+  t.w = unhex(t.w);
+  t.b = unhex(t.b);
+  t.sig = unhex(t.sig);
+  t.pk = unhex(t.pk);
+  return t;
+}
+
+static u32 run_tx(const TxIn& t) {
+  uint8_t blk[64];
+  return check_tx(t.w.data(), (u32)t.w.size(), t.b.data(), (u32)t.b.size(), t.act, t.sig.data(), (u32)t.sig.size(),
+                  t.pk.data(), (u32)t.pk.size(), t.turn, gtab().data(), BlkRef{blk, 4});
+}
+
+// "timed R": only the verify loop is inside the clock (no process start-up,
+// no G-table build, no parsing)
+static void timed(int reps) {
+  std::vector<TxIn> txs;
+  std::string line;
+  while (std::getline(std::cin, line)) {
+    std::istringstream in(line);
+    std::string op;
+    in >> op;
+    if (op == "end") break;
+    if (op == "tx") txs.push_back(parse_tx(in));
+  }
+  gtab();
+  std::vector<u32> v(txs.size());
+  u32 sink = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int r = 0; r < reps; ++r)
+    for (size_t i = 0; i < txs.size(); ++i) {
+      v[i] = run_tx(txs[i]);
+      sink += v[i];
+    }
+  const auto t1 = std::chrono::steady_clock::now();
+  for (u32 x : v) std::cout << x << "\n";
+  std::cout << "ns " << std::chrono::duration_cast<std::chrono::nanoseconds>(t1 - t0).count() << " " << (sink & 0)
+            << "\n";
+  std::cout.flush();
+}
+
 int main() {
   std::string line;
   while (std::getline(std::cin, line)) {
@@ -52,6 +108,12 @@ int main() {
     std::string op;
     in >> op;
     if (op.empty()) continue;
+    if (op == "timed") {
+      int reps = 1;
+      in >> reps;
+      timed(reps);
+      continue;
+    }
     if (op.rfind("fe_", 0) == 0) {
       std::string a, b;
       in >> a >> b;

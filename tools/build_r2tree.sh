@@ -1,5 +1,5 @@
 #!/bin/bash
-# Rebuilds the round-2 failing tree used by tools/gpu_r3m.sh and tools/gpu_r3n.sh
+# Rebuilds the round-2 failing tree used by tools/sessions/r3/gpu_r3m.sh and gpu_r3n.sh
 # (DESIGN.md section 3.6): commit 3d8df08 in full, its final stage built with
 # the struct-of-arrays parents (-DDC_C2C_SOA=1: k_count3c spills 48 B/lane),
 # under distributed-chess_amd/build/var/r2tree (git-ignored; travels with gpurun).
