@@ -36,7 +36,7 @@ constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
 // shift; A/B diagnostics only: 1 = s_nop 1 ahead of the asm shift, 2 = s_nop 1
 // after it, 3 = plain C shifts.
 #ifndef DC_SHIFT_PAD
-#define DC_SHIFT_PAD 4
+#define DC_SHIFT_PAD 0
 #endif
 #if DC_SHIFT_PAD == 1
 #define DC_SHL_ASM "s_nop 1\n\tv_lshlrev_b64 %0, %1, %2"
@@ -235,6 +235,12 @@ __device__ __forceinline__ u32 select_bit_bf(u64 x, u32 k) {
 __device__ __forceinline__ u64 ballot(bool p) { return __ballot(p); }
 
 __device__ __forceinline__ u32 lane_id() { return __lane_id(); }
+// Number of set bits of the wave mask m below this lane: two v_mbcnt with the
+// mask read straight from its SGPRs (no copy of the mask into VGPRs, no
+// popcount of m & below).
+__device__ __forceinline__ u32 mask_rank(u64 m) {
+  return __builtin_amdgcn_mbcnt_hi((u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((u32)m, 0u));
+}
 
 // DPP lane moves (gfx9 encodings: row_shr:n = 0x110 + n, row_bcast:15 =
 // 0x142, row_bcast:31 = 0x143).  Lanes whose source is outside the row, and

@@ -25,6 +25,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <cstddef>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -1010,6 +1011,12 @@ struct C2cParents {
 #if DC_C2C_DIAGQ && !DC_C2C_REC
 #error "DC_C2C_DIAGQ needs DC_C2C_REC"
 #endif
+// DC_C2C_REUSE = 1: the parent split keeps the side to move's eight slider
+// target sets (its own fills) for the first window's enumeration of the
+// special moves, which otherwise runs the same eight fills again.
+#ifndef DC_C2C_REUSE
+#define DC_C2C_REUSE 1
+#endif
 #if DC_C2C_DIAGQ
 struct alignas(8) C2cRec {
   u64 b0, b1, b2, b3, att, orth;
@@ -1139,6 +1146,8 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   constexpr bool GQ = DC_C2C_DIAGQ && BULK;
   u32* q = sh.queue[w];
 #if DC_C2C_DIAGQ
+  static_assert(offsetof(C2cShared<CAP>, queue_d) == offsetof(C2cShared<CAP>, queue) + sizeof(sh.queue),
+                "queue_d must follow queue");
   u32* qd = sh.queue_d[w];
 #else
   u32* qd = q;
@@ -1146,11 +1155,13 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   u32 cnt = 0, base = 0, diag = 0;
   u64 att = 0, orth = 0, Fs = 0, Ts = 0, simple_leaves = 0;
   u32 nsim = 0;
+  constexpr bool REUSE = GQ && DC_C2C_REUSE;
+  u64 tgt[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (REUSE) slider target sets, compile-time indexed
   sh.put_tag(otid(w), tag);  // (the previous group ended with a barrier)
   if (valid) {
     if constexpr (BULK) {
       ParentSplit ps;
-      ref_parent_split<STM, GQ>(p, ps);
+      ref_parent_split<STM, GQ, REUSE>(p, ps, tgt);
       base = ps.base;
       att = ps.att;
       if constexpr (GQ) {
@@ -1240,15 +1251,19 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     if constexpr (GQ) {
       const bool go = ((((c.o >> t) | (c.o >> f)) & 1) != 0);
       const u64 ef = ballot(full && go), ed = em ^ ef;
-      const u64 below = (1ull << lane) - 1;
       if (full) {
-        if (go) q[qn + (u32)__popcll(ef & below)] = c.e;
-        else qd[qnd + (u32)__popcll(ed & below)] = c.e;
+        // one store through a selected address; the ranks from v_mbcnt on the
+        // SGPR masks (round 4: 20 -> 8 VALU per candidate, tools/bbprof.py)
+        // (qd = q + kQd: sh.queue_d follows sh.queue, so one base address)
+        constexpr u32 kQd = sizeof(sh.queue) / sizeof(u32);
+        u32 rf = mask_rank(ef), rd = mask_rank(ed);
+        asm("" : "+v"(rf), "+v"(rd));  // both ranks, then one select (not a select of the masks)
+        q[go ? qn + rf : kQd + qnd + rd] = c.e;
       }
       qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(ef));
       qnd = __builtin_amdgcn_readfirstlane(qnd + (u32)__popcll(ed));
     } else {
-      if (full) q[qn + (u32)__popcll(em & ((1ull << lane) - 1))] = c.e;
+      if (full) q[qn + mask_rank(em)] = c.e;
       qn = __builtin_amdgcn_readfirstlane(qn + (u32)__popcll(em));
     }
   };
@@ -1293,6 +1308,12 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     // (GQ) and the simple-move masks rebuilt from it and its rays
     // (ref_parent_split's keep), so neither is live across the loop
     auto each_move = [&](auto&& visit) {
+      if constexpr (REUSE) {
+        if (wbase == 0) {  // the norm: the split's masks and fills are still live
+          ref_for_each_special_pre<STM>(sh.board(otid(w)), Fs, Ts, tgt, visit);
+          return;
+        }
+      }
       if constexpr (GQ) {
         const Board pp = sh.board(otid(w));
         u32 unused;

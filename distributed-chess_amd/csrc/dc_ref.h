@@ -438,8 +438,11 @@ struct ParentSplit {
 };
 
 // GROUPS: also orth/diag (ref_count_nonpawn_g) for the group-wise recount.
-template <int STM, bool GROUPS = false>
-__device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r) {
+// TGT: also the side to move's slider target sets per direction (tgt[0..7]
+// in ref_for_each_special's slide order), so the enumeration of the special
+// moves reuses these fills instead of running them again (DC_C2C_REUSE).
+template <int STM, bool GROUPS = false, bool TGT = false>
+__device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r, u64* tgt = nullptr) {
   if constexpr (GROUPS) r.base = ref_count_nonpawn_g<1 - STM>(b, r.att, r.orth, r.diag);
   else r.base = ref_count_nonpawn<1 - STM>(b, r.att);
   const u64 keep = ~(r.att | ref_pawn_sensitive<1 - STM>(b, r.pawn_o));
@@ -471,25 +474,49 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r)
   leap(integral_constant<int, -17>{}, kNotH);
   t += king_moves(s.K, no);
   m += king_moves(s.K & Fs, Ts);
-  auto slide = [&](u64 sl, auto stag, auto mtag) {
+#ifndef DC_C2C_KSKIP
+#define DC_C2C_KSKIP 0
+#endif
+  // KSKIP: the simple moves' fill (from the sliders in Fs) differs from the
+  // full one only where a slider stands on a K square (off Fs); a wave none of
+  // whose lanes has such a slider in the class skips that second fill
+  // (one wave-uniform branch per slider class, ballot)
+  auto slide = [&](u64 sl, auto stag, auto mtag, auto itag, auto two) {
     constexpr int S = decltype(stag)::value;
     constexpr u64 M = decltype(mtag)::value;
     u64 ra, rs;
-    ray_attacks2<S, M>(sl, sl & Fs, e, ra, rs);
-    t += pc(ra & no);
+    if constexpr (decltype(two)::value) {
+      ray_attacks2<S, M>(sl, sl & Fs, e, ra, rs);
+    } else {
+      ra = ray_attacks<S, M>(sl, e);
+      rs = ra;
+    }
+    const u64 rt = ra & no;
+    t += pc(rt);
     m += pc(rs & Ts);
+    if constexpr (TGT) tgt[decltype(itag)::value] = rt;
   };
   using K = std::integral_constant<u64, kAll>;
   using NA = std::integral_constant<u64, kNotA>;
   using NH = std::integral_constant<u64, kNotH>;
-  slide(s.O, integral_constant<int, 8>{}, K{});
-  slide(s.O, integral_constant<int, -8>{}, K{});
-  slide(s.O, integral_constant<int, 1>{}, NA{});
-  slide(s.O, integral_constant<int, -1>{}, NH{});
-  slide(s.D, integral_constant<int, 9>{}, NA{});
-  slide(s.D, integral_constant<int, -9>{}, NH{});
-  slide(s.D, integral_constant<int, 7>{}, NH{});
-  slide(s.D, integral_constant<int, -7>{}, NA{});
+  auto orth = [&](auto two) {
+    slide(s.O, integral_constant<int, 8>{}, K{}, integral_constant<int, 0>{}, two);
+    slide(s.O, integral_constant<int, -8>{}, K{}, integral_constant<int, 1>{}, two);
+    slide(s.O, integral_constant<int, 1>{}, NA{}, integral_constant<int, 2>{}, two);
+    slide(s.O, integral_constant<int, -1>{}, NH{}, integral_constant<int, 3>{}, two);
+  };
+  auto diag = [&](auto two) {
+    slide(s.D, integral_constant<int, 9>{}, NA{}, integral_constant<int, 4>{}, two);
+    slide(s.D, integral_constant<int, -9>{}, NH{}, integral_constant<int, 5>{}, two);
+    slide(s.D, integral_constant<int, 7>{}, NH{}, integral_constant<int, 6>{}, two);
+    slide(s.D, integral_constant<int, -7>{}, NA{}, integral_constant<int, 7>{}, two);
+  };
+  using T2 = std::true_type;
+  using T1 = std::false_type;
+  if (!DC_C2C_KSKIP || __ballot((s.O & ~Fs) != 0) != 0) orth(T2{});
+  else orth(T1{});
+  if (!DC_C2C_KSKIP || __ballot((s.D & ~Fs) != 0) != 0) diag(T2{});
+  else diag(T1{});
   r.n_total = t;
   r.n_simple = m;
 }
@@ -552,6 +579,64 @@ __device__ __forceinline__ void ref_for_each_special(const Board& b, u64 Fs, u64
   slide(ray_attacks<-9, kNotH>(s.D, e) & no, integral_constant<int, 5>{});
   slide(ray_attacks<7, kNotH>(s.D, e) & no, integral_constant<int, 6>{});
   slide(ray_attacks<-7, kNotA>(s.D, e) & no, integral_constant<int, 7>{});
+}
+
+// ref_for_each_special with the slider target sets given (tgt[0..7]: the
+// fills ref_parent_split<STM, G, true> already made); same visiting order.
+template <int STM, class Visit>
+__device__ __forceinline__ void ref_for_each_special_pre(const Board& b, u64 Fs, u64 Ts, const u64* tgt, Visit&& visit) {
+  const Sides s = sides<STM>(b);
+  typedef PawnDir<STM> PD;
+  const u64 no = s.notown, e = s.empty;
+  auto leap = [&](u64 targets, int delta, u64 simple) {
+    targets &= ~simple;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(t - delta, t);
+    }
+  };
+  const u64 push1 = sh<PD::F>(s.P) & e;
+  leap(push1, PD::F, sh<PD::F>(Fs) & Ts);
+  leap(sh<PD::F>(push1 & PD::ROW_AFTER1) & e, 2 * PD::F, sh<2 * PD::F>(Fs) & Ts);
+  leap(sh<PD::CW>(s.P & kNotA) & s.enemy, PD::CW, 0);
+  leap(sh<PD::CE>(s.P & kNotH) & s.enemy, PD::CE, 0);
+  const u64 n = s.N;
+  leap(sh<17>(n & kNotH) & no, 17, sh<17>(Fs) & Ts);
+  leap(sh<15>(n & kNotA) & no, 15, sh<15>(Fs) & Ts);
+  leap(sh<10>(n & kNotGH) & no, 10, sh<10>(Fs) & Ts);
+  leap(sh<6>(n & kNotAB) & no, 6, sh<6>(Fs) & Ts);
+  leap(sh<-6>(n & kNotGH) & no, -6, sh<-6>(Fs) & Ts);
+  leap(sh<-10>(n & kNotAB) & no, -10, sh<-10>(Fs) & Ts);
+  leap(sh<-15>(n & kNotH) & no, -15, sh<-15>(Fs) & Ts);
+  leap(sh<-17>(n & kNotA) & no, -17, sh<-17>(Fs) & Ts);
+  const u64 k = s.K;
+  leap(sh<8>(k) & no, 8, sh<8>(Fs) & Ts);
+  leap(sh<-8>(k) & no, -8, sh<-8>(Fs) & Ts);
+  leap(sh<1>(k & kNotH) & no, 1, sh<1>(Fs) & Ts);
+  leap(sh<-1>(k & kNotA) & no, -1, sh<-1>(Fs) & Ts);
+  leap(sh<9>(k & kNotH) & no, 9, sh<9>(Fs) & Ts);
+  leap(sh<7>(k & kNotA) & no, 7, sh<7>(Fs) & Ts);
+  leap(sh<-7>(k & kNotH) & no, -7, sh<-7>(Fs) & Ts);
+  leap(sh<-9>(k & kNotA) & no, -9, sh<-9>(Fs) & Ts);
+  auto slide = [&](u64 targets, auto dtag) {
+    constexpr int D = decltype(dtag)::value;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      const int f = slider_source<D>(s.occ, t);
+      if (((Fs >> f) & (Ts >> t) & 1) == 0) visit(f, t);
+    }
+  };
+  using std::integral_constant;
+  slide(tgt[0], integral_constant<int, 0>{});
+  slide(tgt[1], integral_constant<int, 1>{});
+  slide(tgt[2], integral_constant<int, 2>{});
+  slide(tgt[3], integral_constant<int, 3>{});
+  slide(tgt[4], integral_constant<int, 4>{});
+  slide(tgt[5], integral_constant<int, 5>{});
+  slide(tgt[6], integral_constant<int, 6>{});
+  slide(tgt[7], integral_constant<int, 7>{});
 }
 
 // Runtime side-to-move version.

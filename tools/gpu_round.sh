@@ -43,7 +43,7 @@ if has pmc; then
   pass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" p1 && \
   pass "FETCH_SIZE" p2 && pass "WRITE_SIZE" p3 && \
   pass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" p4 && \
-  pass "VALUBusy" p5 || { tail $O/pmc.err; exit 5; }
+  pass "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE" p5 || { tail $O/pmc.err; exit 5; }
   D8=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d8']['total'])")
   D9=$(python -c "import json;print(json.load(open('tests/golden/ref_deep.json'))['startpos_d9']['total'])")
   python tools/pmc_summary.py $O --json $O/pmc_latest.json --source "rocprofv3 --pmc (4 passes), bench.py $P" \
@@ -62,7 +62,7 @@ if has fidepmc; then
     fpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" f1$leg && \
     fpass "FETCH_SIZE" f2$leg && fpass "WRITE_SIZE" f3$leg && \
     fpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE GRBM_COUNT" f4$leg && \
-    fpass "VALUBusy" f5$leg || { tail $O/pmc.err; exit 8; }
+    fpass "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE" f5$leg || { tail $O/pmc.err; exit 8; }
     mkdir -p $O/$leg && mv $O/pmc_f[1-5]$leg $O/$leg/
   done
   python tools/pmc_summary.py $O/fide7 --json $O/pmc_fide7.json --source "rocprofv3 --pmc (4 passes), bench.py --only fide7" \
@@ -83,7 +83,7 @@ if has txpmc; then
   P="--steps 1 --warmup 0 --no-cpu --profile-only --no-perft --no-replay --tx-steps 1"
   tpass() { local c=$1 t=$2; step "pmc $t"; timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err; }
   tpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" t1 && \
-  tpass "FETCH_SIZE" t2 && tpass "WRITE_SIZE" t3 && tpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" t4 && tpass "VALUBusy" t5 || { tail $O/pmc.err; exit 7; }
+  tpass "FETCH_SIZE" t2 && tpass "WRITE_SIZE" t3 && tpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" t4 && tpass "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE" t5 || { tail $O/pmc.err; exit 7; }
   mkdir -p $O/tx && mv $O/pmc_t[1-5] $O/tx/
   python tools/pmc_summary.py $O/tx --json $O/pmc_tx.json --tx-units 262144 --source "rocprofv3 --pmc, bench.py $P" > $O/pmc_tx.txt
   python - <<'PY'

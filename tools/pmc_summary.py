@@ -13,8 +13,16 @@ Per kernel record (units = the kernel's work units per dispatch, from --units):
                            (rocprof's VALUUtilization: active lanes per VALU op)
   lds_conflict_per_lds_cycle = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS
   wait_frac              = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
-  valu_busy              = rocprof's derived VALUBusy / 100: cycles the VALU pipes
-                           are busy (half-rate ops count twice) per available cycle
+  dual_issue_frac        = 2 x SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU: the share of
+                           VALU instructions issued in a same-quad-cycle pair
+  valu_issue_slots_per_launch = (SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / 1024 SIMDs:
+                           VALU issue slots (quad-cycles) one SIMD spends per
+                           launch; x 4.34 cycles (the measured single-issue cost
+                           at 4 waves/SIMD, profiles/r04/issue_costs.json) over the
+                           kernel's cycles = the VALU issue-slot occupancy bench.py
+                           reports.  (rocprof's VALUBusy is not used: its
+                           SQ_ACTIVE_INST_VALU counts one quad-cycle per instruction,
+                           so on gfx950 it is 2 x the issue fraction by construction.)
 bench.py turns these into fractions of the 78.6 T lane-op/s issue peak with the
 kernel's live HIP-event time.
 
@@ -68,8 +76,9 @@ def derived(c, units):
         r["lds_conflict_per_lds_cycle"] = c["SQ_LDS_BANK_CONFLICT"] / c["SQ_ACTIVE_INST_LDS"]
     if c.get("SQ_WAVE_CYCLES") and "SQ_WAIT_INST_ANY" in c:
         r["wait_frac"] = c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"]
-    if "VALUBusy" in c:
-        r["valu_busy"] = c["VALUBusy"] / 100.0
+    if c.get("SQ_INSTS_VALU") and "SQ_ACTIVE_INST_VALU2" in c:
+        r["dual_issue_frac"] = 2 * c["SQ_ACTIVE_INST_VALU2"] / c["SQ_INSTS_VALU"]
+        r["valu_issue_slots_per_launch"] = (c["SQ_INSTS_VALU"] - c["SQ_ACTIVE_INST_VALU2"]) / 1024
     if c.get("SQ_INSTS_VALU") and "SQ_INSTS_SALU" in c:
         r["salu_per_valu"] = c["SQ_INSTS_SALU"] / c["SQ_INSTS_VALU"]
     return r

@@ -63,6 +63,10 @@ __global__ __launch_bounds__(256) void k(unsigned long long* cyc, unsigned* out,
       if constexpr (MODE == 26) OP4("v_perm_b32 %0, %0, %4, %5", "v_perm_b32 %1, %1, %5, %4", "v_perm_b32 %2, %2, %4, %5", "v_perm_b32 %3, %3, %5, %4");
       if constexpr (MODE == 27) OP4("v_mul_lo_u32 %0, %0, %4", "v_mul_lo_u32 %1, %1, %5", "v_mul_lo_u32 %2, %2, %4", "v_mul_lo_u32 %3, %3, %5");
       if constexpr (MODE == 28) OP4("v_xad_u32 %0, %0, %4, %5", "v_xad_u32 %1, %1, %5, %4", "v_xad_u32 %2, %2, %4, %5", "v_xad_u32 %3, %3, %5, %4");
+      // selects in their real context: the mask written by a compare just before
+      if constexpr (MODE == 30) OP4C("v_cmp_gt_u32_e32 vcc, %0, %4", "v_cndmask_b32_e32 %1, %1, %5, vcc", "v_cmp_gt_u32_e32 vcc, %2, %4", "v_cndmask_b32_e32 %3, %3, %5, vcc", "vcc");
+      if constexpr (MODE == 31) OP4C("v_cmp_gt_u32_e64 s[2:3], %0, %4", "v_cndmask_b32_e64 %1, %1, %5, s[2:3]", "v_cmp_gt_u32_e64 s[4:5], %2, %4", "v_cndmask_b32_e64 %3, %3, %5, s[4:5]", "s2", "s3", "s4", "s5");
+      if constexpr (MODE == 32) OP4C("s_mov_b64 vcc, -1", "v_cndmask_b32_e32 %1, %1, %5, vcc", "v_cndmask_b32_e32 %2, %2, %4, vcc", "v_cndmask_b32_e32 %3, %3, %5, vcc", "vcc");
       if constexpr (MODE == 29) OP4C("v_readfirstlane_b32 s2, %0", "v_add_u32_e32 %1, %5, %1", "v_readfirstlane_b32 s3, %2", "v_add_u32_e32 %3, %5, %3", "s2", "s3");
     }
   }
@@ -79,8 +83,9 @@ static const char* kName[] = {
     "v_not_b32_e32", "v_or3_b32", "v_lshl_or_b32", "v_cmp_e32 + v_add_e32", "v_sub/subrev_u32_e32",
     "v_max/min_u32_e32", "v_bcnt + v_and/or (mix)", "v_lshl_b64 + v_bitop3 (mix)", "v_mbcnt_lo/hi",
     "v_add_co/addc_co_e32", "v_lshl_add_u32", "v_and_or_b32", "v_perm_b32", "v_mul_lo_u32", "v_xad_u32",
-    "v_readfirstlane + v_add (mix)"};
-constexpr int kModes = 30;
+    "v_readfirstlane + v_add (mix)", "v_cmp_e32 -> v_cndmask_b32_e32 (vcc)", "v_cmp_e64 -> v_cndmask_b32_e64 (sgpr)",
+    "s_mov vcc -> 3x v_cndmask_b32_e32"};
+constexpr int kModes = 33;
 
 template <int M>
 static void run(int W, unsigned long long* d_cyc, unsigned* out, unsigned long long* h_cyc, int lds_bytes) {
