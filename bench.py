@@ -41,6 +41,10 @@ HBM_PEAK_GBPS = 8000.0
 
 # MI355X (gfx950): 256 CUs x 4 SIMD-32 x 32 lanes per clock x 2.4 GHz (MI355X_MICROARCH.md).
 VALU_PEAK_LANE_OPS = 256 * 4 * 32 * 2.4e9
+CLOCK_HZ = 2.4e9
+# SIMD cycles per VALU issue slot (a single-issue instruction or a dual-issued
+# pair) at 4 waves/SIMD: v_bcnt_u32_b32 stream, profiles/r04/issue_costs.json
+ISSUE_SLOT_CYCLES = 4.34
 # W = int VALU lane-ops per unit, FROZEN from the first parity-passing kernels'
 # rocprofv3 PMC passes (SQ_INSTS_VALU x 64 / units; DESIGN.md "Roofline"):
 #   perft final stage (k_count2, perft(6)): 37,766,248 x 64 / 120,909,581 = 20.0 per leaf
@@ -295,10 +299,19 @@ def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
       frac_int          = rate x W_int / peak with W_int = (SQ_INSTS_VALU_INT32 +
                           SQ_INSTS_VALU_INT64) x 64 / units: SURVEY §8d's and
                           BASELINE.md §3's INT32 VALU fraction;
-      valu_busy         = rocprof VALUBusy / 100 (PMC pass, same kernel): the
-                          VALU pipes' busy cycles, where half-rate ops (64-bit
-                          shifts, v_bcnt, VOP3 selects) count twice -- the
-                          pipe occupancy the issue fraction understates.
+      valu_slot_occupancy = the VALU issue slots the kernel takes per SIMD
+                          ((SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2) / 1024: one
+                          quad-cycle per single instruction or dual-issued pair)
+                          x 4.34 cycles each (the measured single-issue cost at
+                          4 waves/SIMD, tools/ubench/dual_issue.hip,
+                          profiles/r04/issue_costs.json) / the kernel's SIMD
+                          cycles at 2.4 GHz: ~1 means the VALU issue slots are
+                          all taken (bound by instruction count and pairing);
+      dual_issue_frac   = 2 x SQ_ACTIVE_INST_VALU2 / SQ_INSTS_VALU: the share of
+                          VALU instructions issued as a pair (gfx950 pairs only
+                          simple ops -- add/sub/and/or/xor/mov/not/bitop3 -- of
+                          two waves; shifts, popcounts, selects, 3-source adds
+                          are single-issue).
     W_frozen (the first parity-passing kernel's W) is reported
     beside them as the algorithmic gain W_frozen / W, not as a roofline."""
     w = None
@@ -326,9 +339,14 @@ def valu_roof(kernel, rate, unit_name, w_frozen, pmc_rec, w_key=None):
         if w_int is not None:
             roof[f"W_int_lane_ops_per_{unit_name}"] = w_int
             roof["frac_int"] = rate * w_int / peak
-        for k in ("lds_conflict_per_lds_cycle", "wait_frac", "salu_per_valu", "valu_busy"):
+        for k in ("lds_conflict_per_lds_cycle", "wait_frac", "salu_per_valu", "dual_issue_frac"):
             if k in pmc_rec:
                 roof[k] = pmc_rec[k]
+        slots = pmc_rec.get("valu_issue_slots_per_launch")
+        units = pmc_rec.get("units_per_dispatch")
+        if slots and units and rate:
+            # SIMD cycles of one launch at the live rate: units / rate seconds x 2.4 GHz
+            roof["valu_slot_occupancy"] = slots * ISSUE_SLOT_CYCLES / (units / rate * CLOCK_HZ)
     return roof
 
 

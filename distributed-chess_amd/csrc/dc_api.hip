@@ -118,6 +118,11 @@ struct dc_ctx {
   DBuf<Board> root;
   DBuf<uint16_t> root_meta;
   DBuf<dc::ResultCursor> rcur;  // dc_perft_repeat_device: where the next run's result goes
+  // dc_perft_repeat_device pipelines runs over two contexts: this one takes
+  // the even runs, `twin` (own stream and buffers, created on first use) the
+  // odd ones, so one run's front end overlaps the other's final stage
+  struct dc_ctx* twin = nullptr;
+  hipEvent_t twin_ev[2] = {nullptr, nullptr};
   dc::PerftResult* res_host = nullptr;  // pinned
   u64* replay_host = nullptr;            // pinned: the replay kernel's five counters
   struct HostIo* host_io = nullptr;      // pinned: small validate / apply batches, read and written in place
@@ -386,6 +391,12 @@ int dc_ctx_destroy(dc_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)live_stop(c);
   (void)hipStreamSynchronize(c->stream);
+  if (c->twin) {
+    (void)dc_ctx_destroy(c->twin);
+    c->twin = nullptr;
+  }
+  for (auto& e : c->twin_ev)
+    if (e) (void)hipEventDestroy(e);
   delete c;
   return DC_SUCCESS;
 }
@@ -1659,12 +1670,9 @@ int dc_perft_shard(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth,
 // host round trip between runs.  The first call of a configuration runs it once
 // through perft_impl (host sync), which captures the launch sequence; later
 // runs replay that hipGraph.  Returns once the runs are enqueued.
-int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
-                           uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out) {
-  ENTER(c);
-  if (!pos || (n_runs && !d_out) || rules > DC_RULES_FIDE || n_shards == 0 || shard >= n_shards || pos->stm > 1)
-    return DC_EINVAL;
-  if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
+// n_runs runs on context c, the results at d_out + 258 (idx0 + stride i).
+static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
+                       uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out, u32 idx0, u32 stride) {
   if (n_runs == 0) return DC_SUCCESS;
   HIP_TRY(c->rcur.ensure(1));  // before the key: an allocation moves the epoch
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
@@ -1679,7 +1687,7 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     if (c->last_exact) {
       // speculative capacities overflow for this configuration: exact runs
       // (one host sync per level), each result still left on the device
-      HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out)));
+      HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out), idx0, stride));
       for (u32 i = 0; i < n_runs; ++i) {
         bool hs = false;
         e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs);
@@ -1723,7 +1731,7 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
-  HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out)));
+  HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out), idx0, stride));
   for (u32 i = 0; i < n_runs; ++i) {
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
@@ -1735,6 +1743,39 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     }
   }
   return DC_SUCCESS;
+}
+
+int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
+                           uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out) {
+  ENTER(c);
+  if (!pos || (n_runs && !d_out) || rules > DC_RULES_FIDE || n_shards == 0 || shard >= n_shards || pos->stm > 1)
+    return DC_EINVAL;
+  if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
+  if (n_runs == 0) return DC_SUCCESS;
+  // one run, or kernel timing (profiling reads per-launch events on c's
+  // stream): all runs on this context
+#ifndef DC_REPEAT_PIPE
+#define DC_REPEAT_PIPE 1  // (A/B builds: 0 = every run on this context)
+#endif
+  if (n_runs < 2 || c->profiling || !DC_REPEAT_PIPE)
+    return repeat_runs(c, rules, pos, depth, split_depth, shard, n_shards, n_runs, d_out, 0, 1);
+  // Two contexts, every other run each: the runs are independent (own levels,
+  // words, result block), and the twin's stream waits for what this stream had
+  // queued before the call, this stream for the twin's runs after it -- so to
+  // the caller the call is ordered on this context's stream as before.
+  if (!c->twin) {
+    const int e = dc_ctx_create(c->device, &c->twin);
+    if (e != DC_SUCCESS) return e;
+    for (auto& ev : c->twin_ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+  }
+  dc_ctx* t = c->twin;
+  HIP_TRY(hipEventRecord(c->twin_ev[0], c->stream));
+  HIP_TRY(hipStreamWaitEvent(t->stream, c->twin_ev[0], 0));
+  int e = repeat_runs(c, rules, pos, depth, split_depth, shard, n_shards, (n_runs + 1) / 2, d_out, 0, 2);
+  if (e == DC_SUCCESS) e = repeat_runs(t, rules, pos, depth, split_depth, shard, n_shards, n_runs / 2, d_out, 1, 2);
+  HIP_TRY(hipEventRecord(c->twin_ev[1], t->stream));
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->twin_ev[1], 0));
+  return e;
 }
 
 int dc_ctx_synchronize(dc_ctx* c) {

@@ -1066,63 +1066,81 @@ __device__ __forceinline__ void sys_store(u32* p, u32 v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// One request: lane e < n validates (applies) entry e; `fld(k, e)` reads
+// field k of entry e.  Writes the stamped response words.
+template <class F>
+__device__ __forceinline__ void live_serve(LiveBox* box, u32 stamp, u32 n, bool apply, bool fide, u32 lane, F&& fld) {
+  if (lane >= n) return;
+  DevPos p;
+  for (int q = 0; q < 4; ++q)
+    p.bb[q] = (u64)fld(4 * q) | ((u64)fld(4 * q + 1) << 16) | ((u64)fld(4 * q + 2) << 32) |
+              ((u64)fld(4 * q + 3) << 48);
+  const u32 f16 = fld(16);
+  p.stm = (uint8_t)(f16 & 0xFF);
+  p.castle = (uint8_t)(f16 >> 8);
+  p.ep = (int8_t)(uint8_t)fld(17);
+  p.r0 = 0;
+  p.r1 = 0;
+  const uint16_t mv = (uint16_t)fld(18);
+  uint8_t v = 0, info = 0;
+  if (apply) {
+    if (fide) apply_fide_one(&p, &mv, 0, &v, &info);
+    else apply_ref_one(&p, &mv, 0, &v, &info);
+    const u32 sh = stamp << 16;
+    for (int q = 0; q < 4; ++q)
+      for (int h = 0; h < 4; ++h)
+        sys_store(&box->resp[(1 + 4 * q + h) * n + lane], sh | (u32)((p.bb[q] >> (16 * h)) & 0xFFFF));
+    sys_store(&box->resp[17 * n + lane], sh | p.stm | ((u32)p.castle << 8));
+    sys_store(&box->resp[18 * n + lane], sh | (u32)(uint8_t)p.ep);
+  } else {
+    const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+    v = (uint8_t)(fide ? fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), mv) : ref_verdict(b, p.stm & 1, mv));
+  }
+  sys_store(&box->resp[lane], (stamp << 16) | v | ((u32)info << 8));
+}
+
 __global__ __launch_bounds__(64) void k_live(LiveBox* box, u32 seq, u64 lease_ticks) {
   __shared__ uint16_t fld[kLiveFields * kLiveMax];
+  // a poll reads the request's first kPoll words (an n = 1 request is 20) and
+  // the stop word: two 64-byte lines, not the 256 bytes of all 64 lanes
+  constexpr u32 kPoll = 1 + kLiveFields + 3;
   const u32 lane = threadIdx.x;
   u64 t_last = wall_clock64();
-  for (;;) {
+  for (u32 spin = 1;; ++spin) {
     const u32 stamp = live_stamp(seq + 1);
-    const u32 w0 = sys_load(&box->req[lane]);
-    const u32 ctl = sys_load(&box->ctl);
+    const u32 w0 = lane < kPoll ? sys_load(&box->req[lane]) : (lane == kPoll ? sys_load(&box->ctl) : 0u);
     const u32 hdr = lane_bcast(w0, 0);
     if ((hdr >> 16) == stamp) {
       const u32 n = min(max(hdr & 127u, 1u), kLiveMax);
       const bool apply = (hdr >> 7) & 1, fide = (hdr >> 8) & 1;
       const u32 words = 1 + kLiveFields * n;
-      bool torn = false;
-      for (u32 base = 0; base < words; base += 64) {
-        const u32 j = base + lane;
-        const u32 w = base == 0 ? w0 : (j < words ? sys_load(&box->req[j]) : 0u);
-        if (j < words) {
-          torn |= (w >> 16) != stamp;
-          if (j >= 1) fld[j - 1] = (uint16_t)w;
+      if (n == 1) {
+        // the live consensus call: entry 0's fields are words 1..19, in the
+        // lanes that polled them; lane 0 reads them across lanes (no LDS)
+        if (__ballot(lane < words && (w0 >> 16) != stamp)) continue;  // still being written
+        live_serve(box, stamp, 1, apply, fide, lane, [&](u32 k) { return lane_bcast(w0, 1 + k) & 0xFFFFu; });
+      } else {
+        bool torn = false;
+        for (u32 base = 0; base < words; base += 64) {
+          const u32 j = base + lane;
+          const u32 w = (base == 0 && lane < kPoll) ? w0 : (j < words ? sys_load(&box->req[j]) : 0u);
+          if (j < words) {
+            torn |= (w >> 16) != stamp;
+            if (j >= 1) fld[j - 1] = (uint16_t)w;
+          }
         }
+        if (__ballot(torn)) continue;  // a request still being written: poll again
+        __syncthreads();
+        live_serve(box, stamp, n, apply, fide, lane, [&](u32 k) -> u32 { return fld[k * n + lane]; });
+        __syncthreads();  // fld is rewritten by the next request
       }
-      if (__ballot(torn)) continue;  // a request still being written: poll again
-      __syncthreads();
-      if (lane < n) {
-        auto f = [&](u32 k) -> u32 { return fld[k * n + lane]; };
-        DevPos p;
-        for (int q = 0; q < 4; ++q)
-          p.bb[q] = (u64)f(4 * q) | ((u64)f(4 * q + 1) << 16) | ((u64)f(4 * q + 2) << 32) | ((u64)f(4 * q + 3) << 48);
-        p.stm = (uint8_t)(f(16) & 0xFF);
-        p.castle = (uint8_t)(f(16) >> 8);
-        p.ep = (int8_t)(uint8_t)f(17);
-        p.r0 = 0;
-        p.r1 = 0;
-        const uint16_t mv = (uint16_t)f(18);
-        uint8_t v = 0, info = 0;
-        if (apply) {
-          if (fide) apply_fide_one(&p, &mv, 0, &v, &info);
-          else apply_ref_one(&p, &mv, 0, &v, &info);
-          const u32 sh = stamp << 16;
-          for (int q = 0; q < 4; ++q)
-            for (int h = 0; h < 4; ++h)
-              sys_store(&box->resp[(1 + 4 * q + h) * n + lane], sh | (u32)((p.bb[q] >> (16 * h)) & 0xFFFF));
-          sys_store(&box->resp[17 * n + lane], sh | p.stm | ((u32)p.castle << 8));
-          sys_store(&box->resp[18 * n + lane], sh | (u32)(uint8_t)p.ep);
-        } else {
-          const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
-          v = (uint8_t)(fide ? fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), mv) : ref_verdict(b, p.stm & 1, mv));
-        }
-        sys_store(&box->resp[lane], (stamp << 16) | v | ((u32)info << 8));
-      }
-      __syncthreads();  // fld is rewritten by the next request
       ++seq;
       t_last = wall_clock64();
       continue;
     }
-    if (ctl == 1 || wall_clock64() - t_last > lease_ticks) break;
+    // the stop word, and the lease on the clock every 16th empty poll
+    if (lane_bcast(w0, kPoll) == 1) break;
+    if ((spin & 15) == 0 && wall_clock64() - t_last > lease_ticks) break;
   }
   if (lane == 0) __hip_atomic_store(&box->state, 2u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }

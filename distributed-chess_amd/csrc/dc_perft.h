@@ -64,11 +64,12 @@ hipError_t launch_slice(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
 // The destination is read from a device-side cursor {base, run index} that the
 // copy advances, so one captured graph (perft + copy) serves every run:
 // launch_set_result_cursor points it at base, run 0.
+// (stride: dc_perft_repeat_device's two pipelined contexts take every other run)
 struct ResultCursor {
   u64* base;
-  u64 idx;
+  u32 idx, stride;
 };
-hipError_t launch_set_result_cursor(hipStream_t st, ResultCursor* cur, u64* base);
+hipError_t launch_set_result_cursor(hipStream_t st, ResultCursor* cur, u64* base, u32 idx0 = 0, u32 stride = 1);
 hipError_t launch_copy_result(hipStream_t st, const PerftResult* res, ResultCursor* cur);
 // Strided shard: every n_shards-th node of the level, gathered to out[0..).
 hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* in_meta, const uint16_t* in_tags,

@@ -43,6 +43,7 @@ struct RefRules {
   // blocks of 256 per CU the level / final-stage kernels are built for
   // (FIDE's legal-move analysis needs the registers of 2: spill-free)
   static constexpr int kMinBlocks = 4;
+  static constexpr int kFinalMinBlocks = 4;  // k_count2b
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32) { return ref_count<STM>(b); }
   template <int STM, class V>
@@ -62,6 +63,9 @@ struct RefRules {
 struct FideRules {
   static constexpr bool kMeta = true;
   static constexpr int kMinBlocks = DC_FIDE_MINB;
+  // k_count2b: 3 blocks/CU (148 VGPRs, 0 B) since the parent is re-read from
+  // LDS for the enumeration (its registers are free across the child loop)
+  static constexpr int kFinalMinBlocks = DC_FIDE_MINB > 3 ? DC_FIDE_MINB : 3;
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32 meta) { return fide_count<STM>(b, meta); }
   template <int STM, class V>
@@ -889,7 +893,7 @@ struct C2bShared {
 };
 
 template <class R, int STM>
-__global__ __launch_bounds__(256, R::kMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
+__global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                     u64* __restrict__ divide) {
   __shared__ C2bShared sh;
@@ -924,7 +928,11 @@ __global__ __launch_bounds__(256, R::kMinBlocks) void k_count2b(const Board* __r
       if (base) __syncthreads();  // previous window fully read
       u32 j = excl;
       if (valid && j < base + kC2bCap && j + cnt > base) {
-        R::template for_each<STM>(p, pm, [&](int f, int t, int promo) {
+        // the parent read back from LDS: p and pm are not live across the
+        // child loop (FIDE fits 4 blocks/CU only with every such VGPR freed)
+        const Board pp = sh.par[tid];
+        const u32 ppm = R::kMeta ? sh.pmeta[tid] : 0u;
+        R::template for_each<STM>(pp, ppm, [&](int f, int t, int promo) {
           if (j >= base && j - base < kC2bCap) sh.slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (tid << 15);
           ++j;
         });
@@ -1752,17 +1760,19 @@ hipError_t launch_gather_shard(hipStream_t st, const Board* in, const uint16_t* 
   return hipGetLastError();
 }
 
-__global__ void k_set_result_cursor(ResultCursor* cur, u64* base) { *cur = ResultCursor{base, 0}; }
+__global__ void k_set_result_cursor(ResultCursor* cur, u64* base, u32 idx0, u32 stride) {
+  *cur = ResultCursor{base, idx0, stride};
+}
 
-hipError_t launch_set_result_cursor(hipStream_t st, ResultCursor* cur, u64* base) {
-  hipLaunchKernelGGL(k_set_result_cursor, dim3(1), dim3(1), 0, st, cur, base);
+hipError_t launch_set_result_cursor(hipStream_t st, ResultCursor* cur, u64* base, u32 idx0, u32 stride) {
+  hipLaunchKernelGGL(k_set_result_cursor, dim3(1), dim3(1), 0, st, cur, base, idx0, stride);
   return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_copy_result(const PerftResult* __restrict__ r, ResultCursor* __restrict__ cur) {
   __shared__ u64 ws[4];
   const ResultCursor rc = *cur;  // every thread reads it before thread 0 advances it
-  u64* __restrict__ out = rc.base + 258 * rc.idx;
+  u64* __restrict__ out = rc.base + 258 * (u64)rc.idx;
   const u32 i = threadIdx.x, nr = r->n_root;
   const u64 v = i < nr ? r->divide[i] : 0;
   out[i] = v;
@@ -1772,7 +1782,7 @@ __global__ __launch_bounds__(256) void k_copy_result(const PerftResult* __restri
   if (i == 0) {
     out[256] = (u64)nr | ((u64)r->overflow << 32);
     out[257] = ws[0] + ws[1] + ws[2] + ws[3];
-    cur->idx = rc.idx + 1;  // after the barrier: all threads hold rc
+    cur->idx = rc.idx + rc.stride;  // after the barrier: all threads hold rc
   }
 }
 

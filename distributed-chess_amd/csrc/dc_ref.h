@@ -475,7 +475,7 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   t += king_moves(s.K, no);
   m += king_moves(s.K & Fs, Ts);
 #ifndef DC_C2C_KSKIP
-#define DC_C2C_KSKIP 0
+#define DC_C2C_KSKIP 1
 #endif
   // KSKIP: the simple moves' fill (from the sliders in Fs) differs from the
   // full one only where a slider stands on a K square (off Fs); a wave none of
