@@ -44,6 +44,7 @@ struct RefRules {
   // (FIDE's legal-move analysis needs the registers of 2: spill-free)
   static constexpr int kMinBlocks = 4;
   static constexpr int kFinalMinBlocks = 4;  // k_count2b
+  static constexpr int kTopThreads = 1024;    // k_expand_top's one workgroup
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32) { return ref_count<STM>(b); }
   template <int STM, class V>
@@ -66,6 +67,9 @@ struct FideRules {
   // k_count2b: 3 blocks/CU (148 VGPRs, 0 B) since the parent is re-read from
   // LDS for the enumeration (its registers are free across the child loop)
   static constexpr int kFinalMinBlocks = DC_FIDE_MINB > 3 ? DC_FIDE_MINB : 3;
+  // k_expand_top: 512 threads (2 waves/SIMD, 256 VGPRs): the legal-move
+  // analysis fits without scratch (1024 threads: 128 VGPRs, 180 B/lane)
+  static constexpr int kTopThreads = 512;
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32 meta) { return fide_count<STM>(b, meta); }
   template <int STM, class V>
@@ -212,6 +216,7 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
                                           PerftResult* res, u64* wsum, u64* s_total, u32* slots, Board* spar,
                                           uint16_t* smeta, uint16_t* stags, u32 ply, u32* gcnt, u32* node_off,
                                           u32* words = nullptr) {
+  constexpr int kTopThreads = R::kTopThreads;  // (shadows the file-wide 1024)
   const u32 t = threadIdx.x;
   DC_TOP_STAMP(ply, 0);
   const bool stage = n <= kTopStage;
@@ -334,13 +339,14 @@ struct TopBufs {
 // One workgroup: root (ply 0) -> ply `target` (1..3).  Intermediate plies go
 // to scratch; the target ply goes to `out` (capacity cap_out), Range out_rng.
 template <class R>
-__global__ __launch_bounds__(kTopThreads) void k_expand_top(const Board* __restrict__ root,
+__global__ __launch_bounds__(R::kTopThreads) void k_expand_top(const Board* __restrict__ root,
                                                              const uint16_t* __restrict__ root_meta, u32 stm0,
                                                              u32 target, TopBufs sb, Board* __restrict__ out,
                                                              uint16_t* __restrict__ out_meta,
                                                              uint16_t* __restrict__ out_tags, u64 cap_out,
                                                              PerftResult* __restrict__ res, Range* __restrict__ out_rng,
                                                              u32* __restrict__ words) {
+  constexpr int kTopThreads = R::kTopThreads;  // (shadows the file-wide 1024)
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
   __shared__ u32 slots[kTopSlots];
@@ -1711,10 +1717,10 @@ hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const
     b.cap[k] = s.cap[k];
   }
   if (rules == 0)
-    hipLaunchKernelGGL(k_expand_top<RefRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, b, out,
+    hipLaunchKernelGGL(k_expand_top<RefRules>, dim3(1), dim3(RefRules::kTopThreads), 0, st, root, root_meta, stm0, target, b, out,
                        out_meta, out_tags, cap_out, res, out_rng, words);
   else
-    hipLaunchKernelGGL(k_expand_top<FideRules>, dim3(1), dim3(kTopThreads), 0, st, root, root_meta, stm0, target, b,
+    hipLaunchKernelGGL(k_expand_top<FideRules>, dim3(1), dim3(FideRules::kTopThreads), 0, st, root, root_meta, stm0, target, b,
                        out, out_meta, out_tags, cap_out, res, out_rng, words);
   return hipGetLastError();
 }

@@ -18,7 +18,7 @@ import dchess
 LLVM = "/opt/rocm/lib/llvm/bin"
 # mangled-name fragments of the kernels that must stay spill-free
 MUST = ("k_count3c", "k_count2c", "k_perft_dfs", "k_replay_ref4", "k_validate_ref", "k_apply_ref",
-        "k_gen_games_ref", "RefRules", "k_verify_tx", "k_live")
+        "k_gen_games_ref", "RefRules", "FideRules", "k_verify_tx", "k_live")
 
 
 def kernel_scratch():
@@ -54,3 +54,23 @@ def test_ref_kernels_are_spill_free():
     assert len(checked) >= 20, sorted(ks)
     spilling = {n: s for n, s in checked.items() if s != 0}
     assert not spilling, spilling
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(LLVM, "llvm-objdump")), reason="no ROCm llvm tools")
+def test_scratch_bounds_and_lane_spills():
+    """tools/scratch_bounds_check.py on every kernel of the built library: no
+    scratch access outside its kernel's private segment, none through a VGPR
+    or untraced SGPR address, no SGPR-spill VGPR written under a partial EXEC
+    (the two mechanisms examined for the round-2 fault,
+    and the address-select that kept the FIDE analysis in scratch)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import scratch_bounds_check as sbc
+    ks = sbc.kernels_from_lib(dchess.LIB_PATH)
+    assert len(ks) >= 40, sorted(ks)
+    bad = {}
+    for name, (lines, priv, dyn) in ks.items():
+        b, lanes, _, _ = sbc.check_kernel(lines, priv, dyn)
+        if b or lanes:
+            bad[name] = (b + lanes)[:3]
+    assert not bad, bad
