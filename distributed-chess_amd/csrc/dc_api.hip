@@ -118,11 +118,6 @@ struct dc_ctx {
   DBuf<Board> root;
   DBuf<uint16_t> root_meta;
   DBuf<dc::ResultCursor> rcur;  // dc_perft_repeat_device: where the next run's result goes
-  // dc_perft_repeat_device pipelines runs over two contexts: this one takes
-  // the even runs, `twin` (own stream and buffers, created on first use) the
-  // odd ones, so one run's front end overlaps the other's final stage
-  struct dc_ctx* twin = nullptr;
-  hipEvent_t twin_ev[2] = {nullptr, nullptr};
   dc::PerftResult* res_host = nullptr;  // pinned
   u64* replay_host = nullptr;            // pinned: the replay kernel's five counters
   struct HostIo* host_io = nullptr;      // pinned: small validate / apply batches, read and written in place
@@ -391,12 +386,6 @@ int dc_ctx_destroy(dc_ctx* c) {
   (void)hipSetDevice(c->device);
   (void)live_stop(c);
   (void)hipStreamSynchronize(c->stream);
-  if (c->twin) {
-    (void)dc_ctx_destroy(c->twin);
-    c->twin = nullptr;
-  }
-  for (auto& e : c->twin_ev)
-    if (e) (void)hipEventDestroy(e);
   delete c;
   return DC_SUCCESS;
 }
@@ -1752,30 +1741,10 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
     return DC_EINVAL;
   if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
   if (n_runs == 0) return DC_SUCCESS;
-  // one run, or kernel timing (profiling reads per-launch events on c's
-  // stream): all runs on this context
-#ifndef DC_REPEAT_PIPE
-#define DC_REPEAT_PIPE 1  // (A/B builds: 0 = every run on this context)
-#endif
-  if (n_runs < 2 || c->profiling || !DC_REPEAT_PIPE)
-    return repeat_runs(c, rules, pos, depth, split_depth, shard, n_shards, n_runs, d_out, 0, 1);
-  // Two contexts, every other run each: the runs are independent (own levels,
-  // words, result block), and the twin's stream waits for what this stream had
-  // queued before the call, this stream for the twin's runs after it -- so to
-  // the caller the call is ordered on this context's stream as before.
-  if (!c->twin) {
-    const int e = dc_ctx_create(c->device, &c->twin);
-    if (e != DC_SUCCESS) return e;
-    for (auto& ev : c->twin_ev) HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-  }
-  dc_ctx* t = c->twin;
-  HIP_TRY(hipEventRecord(c->twin_ev[0], c->stream));
-  HIP_TRY(hipStreamWaitEvent(t->stream, c->twin_ev[0], 0));
-  int e = repeat_runs(c, rules, pos, depth, split_depth, shard, n_shards, (n_runs + 1) / 2, d_out, 0, 2);
-  if (e == DC_SUCCESS) e = repeat_runs(t, rules, pos, depth, split_depth, shard, n_shards, n_runs / 2, d_out, 1, 2);
-  HIP_TRY(hipEventRecord(c->twin_ev[1], t->stream));
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->twin_ev[1], 0));
-  return e;
+  // (round 4 measured alternating the runs over a second context, so one
+  // run's front end would overlap the other's final stage: 1.03 against
+  // 0.53 ms per perft(7) step; not kept)
+  return repeat_runs(c, rules, pos, depth, split_depth, shard, n_shards, n_runs, d_out, 0, 1);
 }
 
 int dc_ctx_synchronize(dc_ctx* c) {

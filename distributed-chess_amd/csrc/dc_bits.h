@@ -31,9 +31,9 @@ constexpr u64 kDiagAnti = 0x0102040810204080ull;  // h1..a8 (x + y == 7)
 // so one 64-bit shift (4 cycles per wave) beats the compiler's habit of
 // splitting it into v_alignbit_b32 + v_lshlrev_b32 once the halves feed
 // 32-bit bitop3s (tools/ubench/vop_rate.hip, profiles/r01/ubench_vop.txt).
-// DC_SHIFT_PAD selects how the shift is written: 4 (shipped since round 4)
-// an opaque SGPR shift amount, see shift_amount; 0 the round-1..3 inline-asm
-// shift; A/B diagnostics only: 1 = s_nop 1 ahead of the asm shift, 2 = s_nop 1
+// DC_SHIFT_PAD selects how the shift is written: 0 (shipped) the inline-asm
+// shift; A/B diagnostics only: 4 = an opaque SGPR shift amount (shift_amount;
+// measured slower in round 4), 1 = s_nop 1 ahead of the asm shift, 2 = s_nop 1
 // after it, 3 = plain C shifts.
 #ifndef DC_SHIFT_PAD
 #define DC_SHIFT_PAD 0
@@ -127,11 +127,46 @@ __device__ __forceinline__ u64 ray_moves(u64 gen, u64 empty, u64 allowed) {
   return and3(sh<S>(gen), M, allowed);
 }
 
+// Per-square attack and line tables (5 KB in device global memory, resident
+// in each CU's vector L1): one vector load replaces a variable 64-bit shift
+// pair, its select and the wrap-file select.  Round 4 (tools/bbprof_inline.py
+// on k_count3c): king_moves was 5.6 % of the kernel's VALU issue cycles and
+// slider_source ~7 %, almost all of it that arithmetic.  DC_ATT_TAB=0 keeps
+// the arithmetic forms (A/B).
+#ifndef DC_ATT_TAB
+#define DC_ATT_TAB 1
+#endif
+struct AttTables {
+  u64 king[64], knight[64];
+  u64 behind[8][64];  // line_behind<D>(t)
+  constexpr AttTables() : king{}, knight{}, behind{} {
+    constexpr int kStep[8][2] = {{1, 0}, {-1, 0}, {0, 1}, {0, -1}, {1, 1}, {-1, -1}, {1, -1}, {-1, 1}};
+    for (int s = 0; s < 64; ++s) {
+      const int x = s >> 3, y = s & 7;
+      for (int dx = -2; dx <= 2; ++dx)
+        for (int dy = -2; dy <= 2; ++dy) {
+          const int X = x + dx, Y = y + dy, ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
+          if (X < 0 || X > 7 || Y < 0 || Y > 7) continue;
+          if (ax <= 1 && ay <= 1 && (ax | ay)) king[s] |= 1ull << (8 * X + Y);
+          if (ax + ay == 3 && ax && ay) knight[s] |= 1ull << (8 * X + Y);
+        }
+      for (int d = 0; d < 8; ++d)  // walk back from s against the slide direction
+        for (int X = x - kStep[d][0], Y = y - kStep[d][1]; X >= 0 && X < 8 && Y >= 0 && Y < 8;
+             X -= kStep[d][0], Y -= kStep[d][1])
+          behind[d][s] |= 1ull << (8 * X + Y);
+    }
+  }
+};
+__constant__ constexpr AttTables kAtt{};
+
 // The squares of the line through t in direction class D, strictly on the
 // side the source of a slider move toward direction D lies (i.e. "behind" t).
 // D: 0 N(+8) 1 S(-8) 2 E(+1) 3 W(-1) 4 NE(+9) 5 SW(-9) 6 NW(+7) 7 SE(-7).
 template <int D>
 __device__ __forceinline__ u64 line_behind(int t) {
+#if DC_ATT_TAB
+  return kAtt.behind[D][t];
+#endif
   const int x = t >> 3, y = t & 7;
   u64 line;
   if constexpr (D == 0 || D == 1) line = kFileA << y;

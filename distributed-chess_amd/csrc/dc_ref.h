@@ -70,6 +70,9 @@ __device__ __forceinline__ u32 king_moves(u64 k, u64 allowed) {
   if ((k & (k - 1)) == 0) {
     if (!k) return 0;
     const int s = lsb(k);
+#if DC_ATT_TAB
+    return pc(kAtt.king[s] & allowed);
+#endif
     constexpr u64 kAtB2 = 0x0000000000070507ull;  // a1 b1 c1 a2 c2 a3 b3 c3 around b2 (9)
     const u64 att = s >= 9 ? (kAtB2 << (s - 9)) : (kAtB2 >> (9 - s));
     const int f = s & 7;
@@ -293,12 +296,18 @@ __device__ __forceinline__ u32 ref_count_nonpawn_g(const Board& b, u64& att, u64
 // Knight and king attack sets of one square: the pattern around c3 / b2
 // shifted to s, the files a shift wraps into masked (king_moves' trick).
 __device__ __forceinline__ u64 knight_att_sq(int s) {
+#if DC_ATT_TAB
+  return kAtt.knight[s];
+#endif
   constexpr u64 kAtC3 = 0x0000000A1100110Aull;  // b1 d1 a2 e2 a4 e4 b5 d5 around c3 (18)
   const u64 a = s >= 18 ? (kAtC3 << (s - 18)) : (kAtC3 >> (18 - s));
   const int f = s & 7;
   return a & (f <= 1 ? kNotGH : (f >= 6 ? kNotAB : kAll));
 }
 __device__ __forceinline__ u64 king_att_sq(int s) {
+#if DC_ATT_TAB
+  return kAtt.king[s];
+#endif
   constexpr u64 kAtB2 = 0x0000000000070507ull;
   const u64 a = s >= 9 ? (kAtB2 << (s - 9)) : (kAtB2 >> (9 - s));
   const int f = s & 7;

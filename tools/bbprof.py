@@ -18,6 +18,11 @@ Subcommands
   blocks IN.s --kernel SUBSTR [--json OUT]
       The kernel's basic blocks with their static instruction classes (the
       block numbering matches `instrument`).
+  lines IN_G.s --kernel SUBSTR --counts COUNTS.json --costs COSTS.json [--orig ORIG.s]
+      Per source line: the VALU issue cycles, instructions and the single-issue
+      share, from an assembly of the same build compiled with
+      -g -gline-tables-only (the .loc comments; the innermost inlined
+      location).  --orig checks that its blocks match the counted build's.
   model IN.s --kernel SUBSTR --counts COUNTS.json [--costs COSTS.json] [--pmc PMC.json]
       Dynamic instruction counts = sum over blocks of executions x static
       instructions; the VALU mix by issue class; predicted SIMD cycles from the
@@ -328,6 +333,59 @@ def model_cmd(args):
     print(s)
 
 
+LOC = re.compile(r"^\s*\.loc\s+\d+\s+\d+\s+\d+.*;\s*(\S+):(\d+):\d+")
+
+
+def lines_cmd(args):
+    lines = open(args.inp).read().split("\n")
+    start, end = find_kernel(lines, args.kernel)
+    blocks = split_blocks(lines, start, end)
+    if args.orig:
+        _, ob = load_blocks(args.orig, args.kernel)
+        sig = lambda bl: [[op for _, op, _ in ins] for _, ins in bl]
+        if sig(ob) != sig(blocks):
+            raise SystemExit("the -g assembly's blocks differ from the counted build's")
+    counts = json.load(open(args.counts))["wave_executions"]
+    costs = json.load(open(args.costs))
+    w = str(args.waves)
+    # the source location in force at each instruction line
+    loc, where = "?", {}
+    for i in range(start, end):
+        m = LOC.match(lines[i])
+        if m:
+            loc = m.group(1).split("/")[-1] + ":" + m.group(2)
+        where[i] = loc
+    agg = collections.defaultdict(lambda: [0.0, 0, 0, 0])  # cycles, valu, single-issue, salu
+    total = 0.0
+    for k, (_, ins) in enumerate(blocks):
+        e = counts[k] if k < len(counts) else 0
+        if not e:
+            continue
+        for i, op, t in ins:
+            cl = classify(op, t)
+            a = agg[where[i]]
+            if cl.startswith("valu:"):
+                c = costs["valu"].get(op, costs["valu_default"])[w]
+                a[0] += e * c
+                a[1] += e
+                a[2] += e if c > 3.0 else 0
+                total += e * c
+            elif cl == "salu":
+                a[3] += e
+    L = max(1, json.load(open(args.counts)).get("launches", 1))
+    rows = sorted(agg.items(), key=lambda x: -x[1][0])
+    out = [{"loc": k, "cycle_share": round(v[0] / total, 4), "valu_per_launch": v[1] // L,
+            "single_issue_frac": round(v[2] / max(1, v[1]), 3), "salu_per_launch": v[3] // L}
+           for k, v in rows if v[0] > 0]
+    if args.json:
+        json.dump({"kernel": kernel_name(lines, start), "rows": out}, open(args.json, "w"), indent=1)
+    acc = 0.0
+    for r in out[:args.top]:
+        acc += r["cycle_share"]
+        print(f"{r['loc']:28s} {100 * r['cycle_share']:6.2f} %  cum {100 * acc:6.2f} %  valu/launch "
+              f"{r['valu_per_launch']:>12,}  single {r['single_issue_frac']:.2f}")
+
+
 def main():
     ap = argparse.ArgumentParser()
     sub = ap.add_subparsers(dest="cmd", required=True)
@@ -348,8 +406,17 @@ def main():
     m.add_argument("--waves", type=int, default=4)
     m.add_argument("--pmc")
     m.add_argument("--json")
+    ln = sub.add_parser("lines")
+    ln.add_argument("inp")
+    ln.add_argument("--kernel", required=True)
+    ln.add_argument("--counts", required=True)
+    ln.add_argument("--costs", required=True)
+    ln.add_argument("--orig")
+    ln.add_argument("--waves", type=int, default=4)
+    ln.add_argument("--top", type=int, default=60)
+    ln.add_argument("--json")
     a = ap.parse_args()
-    {"instrument": instrument, "blocks": blocks_cmd, "model": model_cmd}[a.cmd](a)
+    {"instrument": instrument, "blocks": blocks_cmd, "model": model_cmd, "lines": lines_cmd}[a.cmd](a)
 
 
 if __name__ == "__main__":

@@ -6,7 +6,7 @@ P="${STALL_ARGS:---steps 3 --warmup 1 --no-cpu --profile-only --no-replay} ${BEN
 pass() { local c=$1 t=$2; timeout -s KILL 90 rocprofv3 --pmc $c --output-format csv -d $O/stall_$t -o p -- python bench.py $P > /dev/null 2>> $O/stall.err; }
 pass "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_VALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CYCLES" a && \
 pass "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_LDS_BANK_CONFLICT" b && \
-pass "VALUBusy" c && pass "VALUUtilization" d && pass "FETCH_SIZE" e || { tail $O/stall.err; exit 5; }
+pass "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE" c && pass "VALUUtilization" d && pass "FETCH_SIZE" e || { tail $O/stall.err; exit 5; }
 python - <<'PY'
 import csv, glob, collections
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
