@@ -162,11 +162,12 @@ __constant__ constexpr AttTables kAtt{};
 // The squares of the line through t in direction class D, strictly on the
 // side the source of a slider move toward direction D lies (i.e. "behind" t).
 // D: 0 N(+8) 1 S(-8) 2 E(+1) 3 W(-1) 4 NE(+9) 5 SW(-9) 6 NW(+7) 7 SE(-7).
-template <int D>
+// TAB false: the arithmetic form (the FIDE generator's single-workgroup top
+// plies are latency-bound, and a table load sits on their dependency chain:
+// FIDE suite at depth 5 2.65 -> 2.79 ms with the table, round 4 A/B)
+template <int D, bool TAB = (DC_ATT_TAB != 0)>
 __device__ __forceinline__ u64 line_behind(int t) {
-#if DC_ATT_TAB
-  return kAtt.behind[D][t];
-#endif
+  if constexpr (TAB) return kAtt.behind[D][t];
   const int x = t >> 3, y = t & 7;
   u64 line;
   if constexpr (D == 0 || D == 1) line = kFileA << y;
@@ -186,9 +187,9 @@ __device__ __forceinline__ u64 line_behind(int t) {
 
 // Source square of a slider move toward D that lands on t: the nearest
 // occupied square behind t.
-template <int D>
+template <int D, bool TAB = (DC_ATT_TAB != 0)>
 __device__ __forceinline__ int slider_source(u64 occ, int t) {
-  const u64 c = occ & line_behind<D>(t);
+  const u64 c = occ & line_behind<D, TAB>(t);
   if constexpr ((D & 1) == 0) return msb(c);
   else return lsb(c);
 }

@@ -329,7 +329,7 @@ __device__ __forceinline__ void fide_for_each_move(const Board& b, u32 meta, Vis
     while (targets) {
       const int t = lsb(targets);
       targets &= targets - 1;
-      visit(slider_source<DD>(f.occ, t), t, 0);
+      visit(slider_source<DD, false>(f.occ, t), t, 0);
     }
   };
   slide(ray_attacks<8, kAll>(O, e) & tm, std::integral_constant<int, 0>{});

@@ -71,7 +71,7 @@ __device__ __forceinline__ u32 king_moves(u64 k, u64 allowed) {
     if (!k) return 0;
     const int s = lsb(k);
 #if DC_ATT_TAB
-    return pc(kAtt.king[s] & allowed);
+    return pc(kAtt.king[s & 63] & allowed);  // (& 63: the load may be speculated above the k == 0 exit)
 #endif
     constexpr u64 kAtB2 = 0x0000000000070507ull;  // a1 b1 c1 a2 c2 a3 b3 c3 around b2 (9)
     const u64 att = s >= 9 ? (kAtB2 << (s - 9)) : (kAtB2 >> (9 - s));
@@ -481,8 +481,14 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   leap(integral_constant<int, -10>{}, kNotGH);
   leap(integral_constant<int, -15>{}, kNotA);
   leap(integral_constant<int, -17>{}, kNotH);
-  t += king_moves(s.K, no);
-  m += king_moves(s.K & Fs, Ts);
+  if (DC_ATT_TAB && (s.K & (s.K - 1)) == 0) {  // one king (or none): one attack set for both counts
+    const u64 ka = s.K ? kAtt.king[lsb(s.K) & 63] : 0ull;
+    t += pc(ka & no);
+    m += (s.K & Fs) ? pc(ka & Ts) : 0u;
+  } else {
+    t += king_moves(s.K, no);
+    m += king_moves(s.K & Fs, Ts);
+  }
 #ifndef DC_C2C_KSKIP
 #define DC_C2C_KSKIP 1
 #endif
@@ -530,6 +536,57 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   r.n_simple = m;
 }
 
+// The knight and king moves of ref_for_each_special(_pre), in one order both
+// share.  DC_ENUM_PIECE (round 4): per piece -- the source's attack set from
+// kAtt, its special targets (not both f in Fs and t in Ts) walked in one loop --
+// instead of one loop per direction: a wave pays the slowest lane of every
+// loop it enters, and 16 direction loops (each with its own setup) cost more
+// than 2-3 piece loops (tools/bbprof_inline.py: the enumeration was 25 % of
+// k_count3c's VALU issue cycles).
+#ifndef DC_ENUM_PIECE
+#define DC_ENUM_PIECE 1
+#endif
+template <class Leap, class Visit>
+__device__ __forceinline__ void special_leapers(u64 n, u64 k, u64 no, u64 Fs, u64 Ts, Leap&& leap, Visit&& visit) {
+#if DC_ENUM_PIECE
+  auto piece = [&](int f, u64 att) {
+    const u64 simple = ((Fs >> f) & 1) ? Ts : 0ull;
+    u64 targets = att & no & ~simple;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(f, t);
+    }
+  };
+  for (; n; n &= n - 1) {
+    const int f = lsb(n);
+    piece(f, kAtt.knight[f]);
+  }
+  for (; k; k &= k - 1) {
+    const int f = lsb(k);
+    piece(f, kAtt.king[f]);
+  }
+#else
+  (void)visit;
+  leap(sh<17>(n & kNotH) & no, 17, sh<17>(Fs) & Ts);
+  leap(sh<15>(n & kNotA) & no, 15, sh<15>(Fs) & Ts);
+  leap(sh<10>(n & kNotGH) & no, 10, sh<10>(Fs) & Ts);
+  leap(sh<6>(n & kNotAB) & no, 6, sh<6>(Fs) & Ts);
+  leap(sh<-6>(n & kNotGH) & no, -6, sh<-6>(Fs) & Ts);
+  leap(sh<-10>(n & kNotAB) & no, -10, sh<-10>(Fs) & Ts);
+  leap(sh<-15>(n & kNotH) & no, -15, sh<-15>(Fs) & Ts);
+  leap(sh<-17>(n & kNotA) & no, -17, sh<-17>(Fs) & Ts);
+  leap(sh<8>(k) & no, 8, sh<8>(Fs) & Ts);
+  leap(sh<-8>(k) & no, -8, sh<-8>(Fs) & Ts);
+  leap(sh<1>(k & kNotH) & no, 1, sh<1>(Fs) & Ts);
+  leap(sh<-1>(k & kNotA) & no, -1, sh<-1>(Fs) & Ts);
+  leap(sh<9>(k & kNotH) & no, 9, sh<9>(Fs) & Ts);
+  leap(sh<7>(k & kNotA) & no, 7, sh<7>(Fs) & Ts);
+  leap(sh<-7>(k & kNotH) & no, -7, sh<-7>(Fs) & Ts);
+  leap(sh<-9>(k & kNotA) & no, -9, sh<-9>(Fs) & Ts);
+#endif
+}
+
 // ref_for_each_move<STM> without the simple moves (source in Fs, target in
 // Ts): leaper and pawn classes drop them set-wise before the bit loop (the
 // source of target t is t - delta), slider classes per move once the source
@@ -552,24 +609,7 @@ __device__ __forceinline__ void ref_for_each_special(const Board& b, u64 Fs, u64
   leap(sh<PD::F>(push1 & PD::ROW_AFTER1) & e, 2 * PD::F, sh<2 * PD::F>(Fs) & Ts);
   leap(sh<PD::CW>(s.P & kNotA) & s.enemy, PD::CW, 0);
   leap(sh<PD::CE>(s.P & kNotH) & s.enemy, PD::CE, 0);
-  const u64 n = s.N;
-  leap(sh<17>(n & kNotH) & no, 17, sh<17>(Fs) & Ts);
-  leap(sh<15>(n & kNotA) & no, 15, sh<15>(Fs) & Ts);
-  leap(sh<10>(n & kNotGH) & no, 10, sh<10>(Fs) & Ts);
-  leap(sh<6>(n & kNotAB) & no, 6, sh<6>(Fs) & Ts);
-  leap(sh<-6>(n & kNotGH) & no, -6, sh<-6>(Fs) & Ts);
-  leap(sh<-10>(n & kNotAB) & no, -10, sh<-10>(Fs) & Ts);
-  leap(sh<-15>(n & kNotH) & no, -15, sh<-15>(Fs) & Ts);
-  leap(sh<-17>(n & kNotA) & no, -17, sh<-17>(Fs) & Ts);
-  const u64 k = s.K;
-  leap(sh<8>(k) & no, 8, sh<8>(Fs) & Ts);
-  leap(sh<-8>(k) & no, -8, sh<-8>(Fs) & Ts);
-  leap(sh<1>(k & kNotH) & no, 1, sh<1>(Fs) & Ts);
-  leap(sh<-1>(k & kNotA) & no, -1, sh<-1>(Fs) & Ts);
-  leap(sh<9>(k & kNotH) & no, 9, sh<9>(Fs) & Ts);
-  leap(sh<7>(k & kNotA) & no, 7, sh<7>(Fs) & Ts);
-  leap(sh<-7>(k & kNotH) & no, -7, sh<-7>(Fs) & Ts);
-  leap(sh<-9>(k & kNotA) & no, -9, sh<-9>(Fs) & Ts);
+  special_leapers(s.N, s.K, no, Fs, Ts, leap, visit);
   auto slide = [&](u64 targets, auto dtag) {
     constexpr int D = decltype(dtag)::value;
     while (targets) {
@@ -610,24 +650,7 @@ __device__ __forceinline__ void ref_for_each_special_pre(const Board& b, u64 Fs,
   leap(sh<PD::F>(push1 & PD::ROW_AFTER1) & e, 2 * PD::F, sh<2 * PD::F>(Fs) & Ts);
   leap(sh<PD::CW>(s.P & kNotA) & s.enemy, PD::CW, 0);
   leap(sh<PD::CE>(s.P & kNotH) & s.enemy, PD::CE, 0);
-  const u64 n = s.N;
-  leap(sh<17>(n & kNotH) & no, 17, sh<17>(Fs) & Ts);
-  leap(sh<15>(n & kNotA) & no, 15, sh<15>(Fs) & Ts);
-  leap(sh<10>(n & kNotGH) & no, 10, sh<10>(Fs) & Ts);
-  leap(sh<6>(n & kNotAB) & no, 6, sh<6>(Fs) & Ts);
-  leap(sh<-6>(n & kNotGH) & no, -6, sh<-6>(Fs) & Ts);
-  leap(sh<-10>(n & kNotAB) & no, -10, sh<-10>(Fs) & Ts);
-  leap(sh<-15>(n & kNotH) & no, -15, sh<-15>(Fs) & Ts);
-  leap(sh<-17>(n & kNotA) & no, -17, sh<-17>(Fs) & Ts);
-  const u64 k = s.K;
-  leap(sh<8>(k) & no, 8, sh<8>(Fs) & Ts);
-  leap(sh<-8>(k) & no, -8, sh<-8>(Fs) & Ts);
-  leap(sh<1>(k & kNotH) & no, 1, sh<1>(Fs) & Ts);
-  leap(sh<-1>(k & kNotA) & no, -1, sh<-1>(Fs) & Ts);
-  leap(sh<9>(k & kNotH) & no, 9, sh<9>(Fs) & Ts);
-  leap(sh<7>(k & kNotA) & no, 7, sh<7>(Fs) & Ts);
-  leap(sh<-7>(k & kNotH) & no, -7, sh<-7>(Fs) & Ts);
-  leap(sh<-9>(k & kNotA) & no, -9, sh<-9>(Fs) & Ts);
+  special_leapers(s.N, s.K, no, Fs, Ts, leap, visit);
   auto slide = [&](u64 targets, auto dtag) {
     constexpr int D = decltype(dtag)::value;
     while (targets) {

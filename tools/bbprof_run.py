@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one workload on the instrumented library (tools/bbprof_build.sh) and
 write the per-block wave-execution counts (tools/bbprof.py model input).
-  DCHESS_LIB=.../build/bb/libdchess_bb.so python tools/bbprof_run.py perft7|replay|gen OUT.json
+  DCHESS_LIB=.../build/bb/libdchess_bb.so python tools/bbprof_run.py perft7|fide7|replay|gen OUT.json
 The workload's result is checked against its golden value, so an
 instrumentation that changed the kernel's behaviour fails here."""
 import ctypes as C
@@ -23,7 +23,16 @@ fn = getattr(C.CDLL(dchess.LIB_PATH), f"dc_ab_bbprof_{file}")
 fn.argtypes = [C.c_void_p, C.c_int]
 eng = dchess.Engine(0)
 res = {}
-if work.startswith("perft"):
+if work == "fide7":  # FIDE final stage (k_count2b<FideRules>), published perft(7)
+    pos = dchess.pos_from_fen("rnbqkbnr/pppppppp/8/8/8/8/PPPPPPPP/RNBQKBNR w KQkq - 0 1")
+    eng.perft(pos, 7, rules=dchess.RULES_FIDE)
+    assert fn(None, 1) == 0
+    for _ in range(reps):
+        tot, _, _ = eng.perft(pos, 7, rules=dchess.RULES_FIDE)
+        if tot != 3195901860:
+            raise SystemExit(f"FIDE perft(7) = {tot}: the instrumented kernel changed the result")
+    res["result"] = int(tot)
+elif work.startswith("perft"):
     depth = int(work[5:])
     want = {6: 120909581, 7: 3282734510}[depth]
     eng.perft(dchess.startpos(), depth)  # warm (graphs, buffers)
