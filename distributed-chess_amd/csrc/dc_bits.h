@@ -325,5 +325,8 @@ __device__ __forceinline__ u64 lane_bcast64(u64 v, u32 l) {
 
 // Sum over the wave's 64 lanes, wave-uniform (every lane active).
 __device__ __forceinline__ u64 wave_sum64(u64 v) { return lane_bcast64(wave_incl_scan64(v), 63); }
+// The same when every lane's value is below 2^26 (the sum fits 32 bits): one
+// DPP add per step instead of two moves and a 64-bit add
+__device__ __forceinline__ u32 wave_sum32(u32 v) { return lane_bcast(wave_incl_scan(v), 63); }
 
 }  // namespace dc

@@ -60,7 +60,7 @@ __device__ __forceinline__ void tag_hist_add(u64* hist, u32 tag, u64 v, bool val
   const int leader = lsb(lmask);
   const u32 tag0 = lane_bcast(tag, (u32)leader);
   if (ballot(live && tag != tag0) == 0) {
-    const u64 s = wave_sum64(live ? v : 0);
+    const u64 s = ballot(live && (v >> 26) != 0) ? wave_sum64(live ? v : 0) : (u64)wave_sum32(live ? (u32)v : 0u);
     if ((int)lane_id() == leader) atomicAdd((unsigned long long*)&hist[tag0], (unsigned long long)s);
   } else if (live) {
     atomicAdd((unsigned long long*)&hist[tag], (unsigned long long)v);

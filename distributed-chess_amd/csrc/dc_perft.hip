@@ -118,6 +118,26 @@ __device__ __forceinline__ u32 otid(u32 wave) {
   return t;
 }
 
+// 32-bit counts whose block total fits 32 bits (the final stage's special
+// moves per parent): one DPP add per scan step (round 4: the 64-bit scan was
+// 1.6 % of k_count3c's VALU issue cycles)
+template <int NW>
+__device__ __forceinline__ u32 block_excl_scan32(u32 v, u32* wsum /*LDS[NW]*/, u32* total, u32 w = threadIdx.x >> 6) {
+  const u32 incl = wave_incl_scan(v);
+  if (lane_id() == 63) wsum[w] = incl;
+  __syncthreads();
+  u32 before = 0, all = 0;
+#pragma unroll
+  for (int k = 0; k < NW; ++k) {
+    const u32 x = wsum[k];
+    before += ((u32)k < w) ? x : 0u;
+    all += x;
+  }
+  __syncthreads();
+  *total = all;
+  return before + incl - v;
+}
+
 template <int NW>
 __device__ __forceinline__ u64 block_excl_scan64(u64 v, u64* wsum /*LDS[NW]*/, u64* total,
                                                  u32 w = threadIdx.x >> 6) {
@@ -1192,9 +1212,8 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       base = ref_count_nonpawn<1 - STM>(p, att);
     }
   }
-  u64 total64;
-  const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64, w);
-  const u32 total = (u32)total64;
+  u32 total;  // (at most 256 parents x 218 moves)
+  const u32 excl = block_excl_scan32<4>(cnt, reinterpret_cast<u32*>(sh.wsum), &total, w);
   sh.put(otid(w), p, att, base, tag, orth, diag);
   __syncthreads();
   const u32 tag0 = sh.tag(0);

@@ -85,6 +85,25 @@ __device__ __forceinline__ u32 king_moves(u64 k, u64 allowed) {
          pc(and3(sh<-9>(k), kNotH, allowed));
 }
 
+// Knight moves onto `allowed`: per knight one kAtt row and one popcount (the
+// norm is at most two knights: ~26 VALU against 40 for the eight direction
+// terms).  DC_KNIGHT_TAB=0: the direction terms (A/B).
+#ifndef DC_KNIGHT_TAB
+#define DC_KNIGHT_TAB 1
+#endif
+__device__ __forceinline__ u32 knight_moves(u64 n, u64 allowed) {
+#if DC_KNIGHT_TAB
+  u32 c = 0;
+  for (; n; n &= n - 1) c += pc(kAtt.knight[lsb(n) & 63] & allowed);
+  return c;
+#else
+  return pc(and3(sh<17>(n), kNotA, allowed)) + pc(and3(sh<15>(n), kNotH, allowed)) +
+         pc(and3(sh<10>(n), kNotAB, allowed)) + pc(and3(sh<6>(n), kNotGH, allowed)) +
+         pc(and3(sh<-6>(n), kNotAB, allowed)) + pc(and3(sh<-10>(n), kNotGH, allowed)) +
+         pc(and3(sh<-15>(n), kNotA, allowed)) + pc(and3(sh<-17>(n), kNotH, allowed));
+#endif
+}
+
 // Bulk count of REF moves for the side to move: the number of (from,to) pairs
 // validate_move accepts.  Every term is a popcount over one direction class, so
 // multiplicity is exact (two knights reaching one square count twice).  Wrap
@@ -95,15 +114,11 @@ __device__ __forceinline__ u32 ref_count_sides(const Sides& s) {
   typedef PawnDir<STM> PD;
   const u64 push1 = sh<PD::F>(s.P) & s.empty;
   const u64 push2 = and3(sh<PD::F>(push1), PD::ROW_DBL, s.empty);
-  u32 c = pc(push1) + pc(push2);
+  u32 c = pc(push1 | push2);  // (disjoint: a landing square's mid square is empty)
   c += pc(and3(sh<PD::CW>(s.P), kNotH, s.enemy));  // toward column y-1: wraps land on file h
   c += pc(and3(sh<PD::CE>(s.P), kNotA, s.enemy));  // toward column y+1: wraps land on file a
   const u64 no = s.notown;
-  const u64 n = s.N;
-  c += pc(and3(sh<17>(n), kNotA, no)) + pc(and3(sh<15>(n), kNotH, no));
-  c += pc(and3(sh<10>(n), kNotAB, no)) + pc(and3(sh<6>(n), kNotGH, no));
-  c += pc(and3(sh<-6>(n), kNotAB, no)) + pc(and3(sh<-10>(n), kNotGH, no));
-  c += pc(and3(sh<-15>(n), kNotA, no)) + pc(and3(sh<-17>(n), kNotH, no));
+  c += knight_moves(s.N, no);
   c += king_moves(s.K, no);
   const u64 e = s.empty;
   c += pc(ray_attacks<8, kAll>(s.O, e) & no) + pc(ray_attacks<-8, kAll>(s.O, e) & no);
@@ -276,10 +291,7 @@ __device__ __forceinline__ u32 ref_count_nonpawn_g(const Board& b, u64& att, u64
   // the king first: its several-kings branch would otherwise split a block
   // holding all eight knight shifts live (spills at the 128-VGPR budget)
   u32 c = king_moves(s.K, no);
-  c += pc(and3(sh<17>(n), kNotA, no)) + pc(and3(sh<15>(n), kNotH, no));
-  c += pc(and3(sh<10>(n), kNotAB, no)) + pc(and3(sh<6>(n), kNotGH, no));
-  c += pc(and3(sh<-6>(n), kNotAB, no)) + pc(and3(sh<-10>(n), kNotGH, no));
-  c += pc(and3(sh<-15>(n), kNotA, no)) + pc(and3(sh<-17>(n), kNotH, no));
+  c += knight_moves(n, no);
   asm volatile("" : "+v"(c));  // the leaper terms reduced here, not sunk past the fills
   const u64 a0 = ray_attacks<8, kAll>(s.O, e), a1 = ray_attacks<-8, kAll>(s.O, e);
   const u64 a2 = ray_attacks<1, kNotA>(s.O, e), a3 = ray_attacks<-1, kNotH>(s.O, e);
@@ -339,7 +351,7 @@ __device__ __forceinline__ u32 ref_count_child_diag(const Board& b, int f, int t
   c += pc(ray_moves<7, kNotH>(D, e, no)) + pc(ray_moves<-7, kNotA>(D, e, no));
   const u64 P = and_andn(own, b.b1, b.b2 | b.b3);
   const u64 push1 = sh<PD::F>(P) & e;
-  c += pc(push1) + pc(and3(sh<PD::F>(push1), PD::ROW_DBL, e));
+  c += pc(or_and(push1, sh<PD::F>(push1) & PD::ROW_DBL, e));  // single | double pushes (disjoint)
   c += pc(and3(sh<PD::CW>(P), kNotH, enemy)) + pc(and3(sh<PD::CE>(P), kNotA, enemy));
   const u64 kn = knight_att_sq(t), kg = king_att_sq(t);
   const u64 N = and_andn(own, b.b2, b.b1 | b.b3), K = and_andn(own, b.b1 & b.b2, b.b3);
@@ -363,7 +375,7 @@ __device__ __forceinline__ u32 ref_pawn_count_child(const Board& b, int f, int t
   const u64 enemy_c = (occ & ~own) ^ ft;  // the mover's pieces after the move
   const u64 push1 = sh<PD::F>(P) & empty_c;
   const u64 push2 = and3(sh<PD::F>(push1), PD::ROW_DBL, empty_c);
-  return pc(push1) + pc(push2) + pc(and3(sh<PD::CW>(P), kNotH, enemy_c)) + pc(and3(sh<PD::CE>(P), kNotA, enemy_c));
+  return pc(push1 | push2) + pc(and3(sh<PD::CW>(P), kNotH, enemy_c)) + pc(and3(sh<PD::CE>(P), kNotA, enemy_c));
 }
 
 // ------------------------------------------------ bulk split (k_count2c)
@@ -387,7 +399,7 @@ __device__ __forceinline__ u64 ref_pawn_sensitive(const Board& b, u32& pawn_cnt)
   const u64 cw = sh<PD::CW>(s.P) & kNotH, ce = sh<PD::CE>(s.P) & kNotA;
   const u64 push1 = q1 & s.empty;
   const u64 land = sh<PD::F>(push1) & PD::ROW_DBL;  // landings whose mid is empty
-  pawn_cnt = pc(push1) + pc(land & s.empty) + pc(cw & s.enemy) + pc(ce & s.enemy);
+  pawn_cnt = pc(or_and(push1, land, s.empty)) + pc(cw & s.enemy) + pc(ce & s.enemy);
   return bop3<0xFE>(q1, cw, ce) | land;
 }
 
@@ -463,16 +475,26 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   asm volatile("" : "+v"(e));  // opaque copy: no reuse of the opponent's fill masks
   typedef PawnDir<STM> PD;
   const u64 push1 = sh<PD::F>(s.P) & e, push1s = sh<PD::F>(s.P & Fs) & e;
-  u32 t = pc(push1) + pc(and3(sh<PD::F>(push1), PD::ROW_DBL, e));
-  u32 m = pc(push1s & Ts) + pc(and3(sh<PD::F>(push1s), PD::ROW_DBL, Ts));
+  // single and double pushes land on disjoint squares: one popcount each
+  u32 t = pc(or_and(push1, sh<PD::F>(push1) & PD::ROW_DBL, e));
+  u32 m = pc(bop3<0xA8>(push1s, sh<PD::F>(push1s) & PD::ROW_DBL, Ts));  // (a | b) & c
   t += pc(and3(sh<PD::CW>(s.P), kNotH, s.enemy)) + pc(and3(sh<PD::CE>(s.P), kNotA, s.enemy));
+  using std::integral_constant;
+#if DC_KNIGHT_TAB
+  // per knight: its kAtt row counts toward t and, from a source in Fs, m
+  for (u64 n = s.N; n; n &= n - 1) {
+    const int f = lsb(n) & 63;
+    const u64 a = kAtt.knight[f];
+    t += pc(a & no);
+    m += ((Fs >> f) & 1) ? pc(a & Ts) : 0u;
+  }
+#else
   const u64 n = s.N, ns = s.N & Fs;
   auto leap = [&](auto dtag, u64 guard) {
     constexpr int D = decltype(dtag)::value;
     t += pc(and3(sh<D>(n), guard, no));
     m += pc(and3(sh<D>(ns), guard, Ts));
   };
-  using std::integral_constant;
   leap(integral_constant<int, 17>{}, kNotA);
   leap(integral_constant<int, 15>{}, kNotH);
   leap(integral_constant<int, 10>{}, kNotAB);
@@ -481,6 +503,7 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   leap(integral_constant<int, -10>{}, kNotGH);
   leap(integral_constant<int, -15>{}, kNotA);
   leap(integral_constant<int, -17>{}, kNotH);
+#endif
   if (DC_ATT_TAB && (s.K & (s.K - 1)) == 0) {  // one king (or none): one attack set for both counts
     const u64 ka = s.K ? kAtt.king[lsb(s.K) & 63] : 0ull;
     t += pc(ka & no);

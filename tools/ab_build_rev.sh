@@ -1,0 +1,21 @@
+#!/bin/bash
+# A/B baseline from a git revision: dc_perft.hip (and the headers it
+# includes) as of REV, linked with the working tree's other objects
+# (measurement only; tools/ab_perft_time.py times the libraries).
+#   tools/ab_build_rev.sh NAME REV ["FLAGS"]
+# -> distributed-chess_amd/build/var/NAME/libdchess.so
+set -e
+N=$1; REV=$2; F=${3:-}
+R=$(cd "$(dirname "$0")/.." && pwd)
+T=$(mktemp -d)
+git -C $R archive $REV distributed-chess_amd/csrc include | tar -x -C $T
+cd $R/distributed-chess_amd
+make -s libdchess.so
+HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -I$T/include"
+mkdir -p build/var/$N
+/opt/rocm/bin/hipcc $HIPFLAGS $F -c $T/distributed-chess_amd/csrc/dc_perft.hip -o build/var/$N/dc_perft.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -o build/var/$N/libdchess.so build/var/$N/dc_perft.o \
+  build/dc_moves.o build/dc_hash.o build/dc_txsig.o build/dc_api.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+rm -f build/var/$N/dc_perft.o
+rm -rf $T
+echo "built build/var/$N/libdchess.so (dc_perft.hip at $REV $F)"
