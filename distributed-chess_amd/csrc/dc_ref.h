@@ -529,10 +529,12 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
       ra = ray_attacks<S, M>(sl, e);
       rs = ra;
     }
-    const u64 rt = ra & no;
+    const u64 rt = ra & no, st = rs & Ts;
     t += pc(rt);
-    m += pc(rs & Ts);
-    if constexpr (TGT) tgt[decltype(itag)::value] = rt;
+    m += pc(st);
+    // (TGT) the special targets only: t in Ts is simple iff its source is
+    // in Fs, i.e. iff t is in the fill from the sliders in Fs (rs)
+    if constexpr (TGT) tgt[decltype(itag)::value] = and_andn(ra, no, st);
   };
   using K = std::integral_constant<u64, kAll>;
   using NA = std::integral_constant<u64, kNotA>;
@@ -654,7 +656,8 @@ __device__ __forceinline__ void ref_for_each_special(const Board& b, u64 Fs, u64
 }
 
 // ref_for_each_special with the slider target sets given (tgt[0..7]: the
-// fills ref_parent_split<STM, G, true> already made); same visiting order.
+// special targets of the fills ref_parent_split<STM, G, true> already made,
+// simple ones removed); same visiting order.
 template <int STM, class Visit>
 __device__ __forceinline__ void ref_for_each_special_pre(const Board& b, u64 Fs, u64 Ts, const u64* tgt, Visit&& visit) {
   const Sides s = sides<STM>(b);
@@ -679,8 +682,7 @@ __device__ __forceinline__ void ref_for_each_special_pre(const Board& b, u64 Fs,
     while (targets) {
       const int t = lsb(targets);
       targets &= targets - 1;
-      const int f = slider_source<D>(s.occ, t);
-      if (((Fs >> f) & (Ts >> t) & 1) == 0) visit(f, t);
+      visit(slider_source<D>(s.occ, t), t);  // (tgt holds special targets only)
     }
   };
   using std::integral_constant;
