@@ -1165,6 +1165,9 @@ __device__ __forceinline__ u32 c2c_diag(const C2cShared<CAP>& sh, u32 e) {
 // pawn counts; 7 replaces the counts by statistics (tools/c2c_stats.py);
 // 8 is 0 plus a per-block timeline (tools/c2c_trace.py).  Phases other
 // than 0 are instantiated only in the A/B build (-DDC_AB_KNOBS, libdchess_ab.so).
+#ifndef DC_C2C_POOL
+#define DC_C2C_POOL 1  // pooled final queue drains (0: one partial drain per wave, A/B)
+#endif
 // One group of 256 parents (one per thread; `valid` false for an empty slot):
 // the last two plies below each, added into the block's divide histogram.
 // Called by k_count2c (parents read from a level in HBM) and k_perft_dfs
@@ -1393,6 +1396,50 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       drain();
     }
   }
+#if DC_C2C_POOL
+  // Pooled final drains (round 4): the waves' leftover queue entries (fewer
+  // than 64 of each kind per wave) are gathered into one block list in the
+  // slot area and drained 64 at a time, the chunks dealt to the waves in turn:
+  // ceil(total / 64) drains per kind instead of one partial drain per wave
+  // (the partial final drains were 15 % of k_count3c's VALU issue cycles,
+  // tools/bbprof_inline.py).  The parents' records are still in LDS.
+  {
+    u32* cnt = reinterpret_cast<u32*>(sh.wsum);  // [0..3] full, [4..7] group-wise (the scan is done)
+    __syncthreads();  // every wave is past its last slot read: the slot area is free
+    if (lane == 0) {
+      cnt[w] = qn;
+      cnt[4 + w] = GQ ? qnd : 0u;
+    }
+    __syncthreads();
+    u32 of = 0, od = 0, nf = 0, nd = 0;
+#pragma unroll
+    for (u32 v = 0; v < 4; ++v) {
+      const u32 a = cnt[v], b = cnt[4 + v];
+      of += v < w ? a : 0u;
+      od += v < w ? b : 0u;
+      nf += a;
+      nd += b;
+    }
+    nf = __builtin_amdgcn_readfirstlane(nf);
+    nd = __builtin_amdgcn_readfirstlane(nd);
+    if (lane < qn) sh.slot[of + lane] = q[lane];
+    if (GQ && lane < qnd) sh.slot[nf + od + lane] = qd[lane];
+    __syncthreads();
+    const u32 cf = (nf + 63) / 64, cd = (nd + 63) / 64;
+    for (u32 c = w; c < cf + cd; c += 4) {
+      const bool full = c < cf;  // wave-uniform
+      const u32 k = (full ? c * 64 : nf + (c - cf) * 64) + lane;
+      const bool live = k < (full ? nf : nf + nd);
+      const u32 e2 = live ? sh.slot[k] : 0u;
+      u32 r = 0;
+      if (full) r = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2)) : 0u;
+#if DC_C2C_DIAGQ
+      else r = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_diag<STM>(sh, e2)) : 0u;
+#endif
+      add(e2 >> 15, r, live);
+    }
+  }
+#else
   // drain this wave's queue (par/att of the chunk are still in LDS)
   if (qn) {
     wave_lds_sync();
@@ -1409,6 +1456,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     const u32 k = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_diag<STM>(sh, e2)) : 0u;
     add(e2 >> 15, k, live);
   }
+#endif
 #endif
   tag_hist_add(sh.hist, tag0, acc, true);
   __syncthreads();  // par/att/ptag/slot reused by the next group
