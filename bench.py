@@ -21,6 +21,7 @@ Prints ONE JSON line on rank 0.
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -207,6 +208,9 @@ def cpu_baselines(args, threads, replay_host=None):
     return out
 
 
+REPEAT_BATCH = 8  # runs per batch graph of dc_perft_repeat_device (dc_api.hip kRepeatBatch)
+
+
 def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF, want=None):
     """warmup + exactly `steps` timed perft(depth) steps (barrier + device sync on
     both sides, max over ranks), parity-checked against the golden count.
@@ -226,9 +230,10 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF,
             raise SystemExit(f"parity failure: perft({depth}) = {tot}, expected {want}")
     W = 258  # divide[256], n_root | overflow << 32, total
     # the first dc_perft_repeat_device call of a configuration runs one plain
-    # perft and captures the launch graph: do it here, outside the timed region
-    warm = eng.alloc(W * 8)
-    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, 1, warm, rules=rules)
+    # perft and captures the launch graphs (one run, and a batch of
+    # REPEAT_BATCH runs): do it here, outside the timed region
+    warm = eng.alloc(REPEAT_BATCH * W * 8)
+    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, REPEAT_BATCH, warm, rules=rules)
     eng.synchronize()
     warm.free()
     if d.dist is None:
@@ -533,6 +538,21 @@ def validate_latency(eng, calls=2000):
     finally:
         live.live_validator(0)
         live.close()
+    # the same two paths from a compiled caller (tools/latency_probe.cpp, built
+    # by __graft_entry__.build): how the Rust replica calls the C ABI; Python's
+    # ctypes adds ~3 us per call to the figures above
+    probe = os.path.join(REPO, "tools", "latency_probe")
+    if os.path.exists(probe):
+        try:
+            p = subprocess.run([probe, "5000"], capture_output=True, text=True, timeout=120)
+            r = json.loads(p.stdout.strip().splitlines()[-1])
+            if r.get("parity") is not True:
+                raise SystemExit("parity failure: latency_probe verdicts")
+            out["c_abi"] = {"launched": r["launched"], "live": r["live"], "calls": r["calls"],
+                            "note": "tools/latency_probe: steady_clock around each dc_validate_batch(n=1) call "
+                                    "of a compiled C++ caller (no Python between the clock and the ABI)"}
+        except (subprocess.SubprocessError, ValueError, KeyError, IndexError) as e:
+            out["c_abi"] = {"error": str(e)[:200]}
     return out
 
 

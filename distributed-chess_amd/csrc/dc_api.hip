@@ -146,6 +146,10 @@ struct dc_ctx {
   // dc_perft_repeat_device's graph: the same sequence without the root upload
   // and the result readback (the root stays on the device between runs)
   hipGraphExec_t rgraph = nullptr;
+  // ... and kRepeatBatch runs in one graph: consecutive graph launches leave
+  // ~8.6 us between one graph's last kernel and the next graph's first
+  // (rocprofv3 kernel trace, round 4), kernels within a graph none
+  hipGraphExec_t rgraph_batch = nullptr;
   PerftKey rkey{};
   // the last perft_impl needed the exact (host-sized) rerun: its speculative
   // level capacities overflow, so dc_perft_repeat_device must not replay them
@@ -209,6 +213,7 @@ struct dc_ctx {
     slice_ctr.release();
     if (pgraph) (void)hipGraphExecDestroy(pgraph);
     if (rgraph) (void)hipGraphExecDestroy(rgraph);
+    if (rgraph_batch) (void)hipGraphExecDestroy(rgraph_batch);
     if (res_host) (void)hipHostFree(res_host);
     if (replay_host) (void)hipHostFree(replay_host);
     if (host_io) (void)hipHostFree(host_io);
@@ -1660,6 +1665,9 @@ int dc_perft_shard(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth,
 // through perft_impl (host sync), which captures the launch sequence; later
 // runs replay that hipGraph.  Returns once the runs are enqueued.
 // n_runs runs on context c, the results at d_out + 258 (idx0 + stride i).
+// Runs per batch graph of dc_perft_repeat_device (see dc_ctx::rgraph_batch).
+constexpr u32 kRepeatBatch = 8;
+
 static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
                        uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out, u32 idx0, u32 stride) {
   if (n_runs == 0) return DC_SUCCESS;
@@ -1667,6 +1675,25 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
   dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
                        g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
   const bool graphable = !c->profiling && perft_graphs_enabled();
+  // capture `runs` runs of the sequence back to back (the result copy is part
+  // of the graph: its destination is the cursor)
+  auto capture = [&](u32 runs, hipGraphExec_t* out) {
+    if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) != hipSuccess) return false;
+    bool hs = false;
+    int ce = DC_SUCCESS;
+    for (u32 r = 0; r < runs && ce == DC_SUCCESS && !hs; ++r) {
+      ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
+      if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
+    }
+    hipGraph_t g = nullptr;
+    const hipError_t ee = hipStreamEndCapture(c->stream, &g);
+    const bool ok = ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
+                    hipGraphInstantiate(out, g, nullptr, nullptr, 0) == hipSuccess;
+    if (!ok) *out = nullptr;
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return ok;
+  };
   if (!c->root_host || !(graphable && c->rgraph && c->rkey == key)) {
     // a plain run (host sync) sizes the buffers and stages the root; then the
     // sequence is captured without the root upload and the readback
@@ -1687,25 +1714,18 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
     }
     key.epoch = g_alloc_epoch.load();
     if (graphable) {
-      if (c->rgraph) {
-        (void)hipGraphExecDestroy(c->rgraph);
-        c->rgraph = nullptr;
+      for (hipGraphExec_t* ge : {&c->rgraph, &c->rgraph_batch}) {
+        if (*ge) (void)hipGraphExecDestroy(*ge);
+        *ge = nullptr;
       }
-      if (hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-        bool hs = false;
-        // the result copy is part of the graph: its destination is the cursor
-        int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
-        if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
-        hipGraph_t g = nullptr;
-        const hipError_t ee = hipStreamEndCapture(c->stream, &g);
-        if (ce == DC_SUCCESS && ee == hipSuccess && !hs && g && key.epoch == g_alloc_epoch.load() &&
-            hipGraphInstantiate(&c->rgraph, g, nullptr, nullptr, 0) == hipSuccess)
-          c->rkey = key;
-        else
-          c->rgraph = nullptr;
-        if (g) (void)hipGraphDestroy(g);
+      if (capture(1, &c->rgraph)) {
+        c->rkey = key;
+        if (n_runs >= kRepeatBatch) (void)capture(kRepeatBatch, &c->rgraph_batch);
       }
       (void)hipGetLastError();
+    } else if (c->rgraph_batch) {
+      (void)hipGraphExecDestroy(c->rgraph_batch);
+      c->rgraph_batch = nullptr;
     }
   }
   const bool use_graph = graphable && c->rgraph && c->rkey == key;
@@ -1721,7 +1741,15 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
     HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
   HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out), idx0, stride));
-  for (u32 i = 0; i < n_runs; ++i) {
+  u32 i = 0;
+  if (use_graph && n_runs >= kRepeatBatch && !c->rgraph_batch && c->rgraph) {
+    // the key's one-run graph exists but no batch graph yet (an earlier call
+    // had fewer runs): capture it now
+    (void)capture(kRepeatBatch, &c->rgraph_batch);
+  }
+  if (use_graph && c->rgraph_batch)
+    for (; i + kRepeatBatch <= n_runs; i += kRepeatBatch) HIP_TRY(hipGraphLaunch(c->rgraph_batch, c->stream));
+  for (; i < n_runs; ++i) {
     if (use_graph) {
       HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
     } else {

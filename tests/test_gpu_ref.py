@@ -429,6 +429,25 @@ def test_perft_repeat_device(engine, depth, n_shards):
     assert int(res[0, 257]) == 197742 and int(res[1, 257]) == want
 
 
+def test_perft_repeat_device_batches(engine):
+    """Runs past the batch size go through the 8-run batch graph (captured
+    lazily on the first call with >= 8 runs), the rest through the one-run
+    graph; every run's result lands at its own slot, also after the root
+    position changes between calls."""
+    W = 258
+    s = dchess.startpos()
+    mid = dchess.pos_from_fen("rnbqkbnr/pppp1ppp/8/4p3/4P3/8/PPPP1PPP/RNBQKBNR w - - 0 2")
+    want_mid, _, _ = engine.perft(mid, 5)
+    want_s = 4896998  # REF perft(5) of startpos (tests/golden)
+    for pos, want, runs in ((s, want_s, 2), (s, want_s, 19), (mid, want_mid, 9), (s, want_s, 8)):
+        buf = engine.alloc(runs * W * 8)
+        engine.perft_repeat_device(pos, 5, 3, 0, 1, runs, buf)
+        engine.synchronize()
+        res = buf.download(np.uint64, runs * W).reshape(runs, W)
+        buf.free()
+        assert (res[:, 257] == want).all(), res[:, 257]
+
+
 def test_perft_repeat_device_profiling_then_other_position(engine):
     """With profiling on, dc_perft_repeat_device enqueues plain (non-graph) runs,
     each copying the pinned root block when it executes; a perft of another

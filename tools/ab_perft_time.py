@@ -26,8 +26,8 @@ REF7 = 3282734510
 eng = dchess.Engine(0)
 def timed(pos, depth, steps, rules, want):
     W = 258
-    warm = eng.alloc(W * 8)
-    eng.perft_repeat_device(pos, depth, 3, 0, 1, 1, warm, rules=rules)
+    warm = eng.alloc(8 * W * 8)  # 8 runs: also captures the batch graph (kRepeatBatch)
+    eng.perft_repeat_device(pos, depth, 3, 0, 1, 8, warm, rules=rules)
     eng.synchronize()
     warm.free()
     buf = eng.alloc(steps * W * 8)
