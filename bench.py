@@ -232,8 +232,9 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF,
     # the first dc_perft_repeat_device call of a configuration runs one plain
     # perft and captures the launch graphs (one run, and a batch of
     # REPEAT_BATCH runs): do it here, outside the timed region
-    warm = eng.alloc(REPEAT_BATCH * W * 8)
-    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, REPEAT_BATCH, warm, rules=rules)
+    nw = REPEAT_BATCH if steps >= REPEAT_BATCH else 1  # (fewer steps never launch the batch graph)
+    warm = eng.alloc(nw * W * 8)
+    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, nw, warm, rules=rules)
     eng.synchronize()
     warm.free()
     if d.dist is None:
@@ -836,23 +837,33 @@ def main():
     # ------------------------------------------------- perft (headline: depth 7)
     p6 = p8 = p9 = None
     leaves, dt, ks = 0, 0.0, None
+    def note(leg):  # one progress line per leg on stderr (long profiler passes stay visibly alive)
+        if d.rank == 0:
+            print(f"[bench] {leg} {time.strftime('%H:%M:%S')}", file=sys.stderr, flush=True)
+
     if "perft" in legs:
+        note("perft")
         leaves, dt = timed_perft(eng, d, args, pos, args.depth, args.steps, args.warmup)
         ks = profiled_perft(eng, d, args, pos, args.depth, args.steps)
     # perft(6) (BASELINE configs[1]) on the same engine and method, secondary
     if "perft6" in legs:
+        note("perft6")
         l6, dt6 = timed_perft(eng, d, args, pos, 6, 4 * args.steps, args.warmup)
         p6 = {"value": l6 / dt6, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt6 / (4 * args.steps),
               "steps": 4 * args.steps, "workload": "perft(startpos, 6) RULES_REF, frontier split at ply 3",
               "scaling": "strong"}
     if "perft8" in legs:
+        note("perft8")
         p8 = perft8_leg(eng, d, args, pos)
     if "perft9" in legs:
+        note("perft9")
         p9 = perft9_leg(eng, d, args, pos)
     f7 = fs = None
     if "fide7" in legs:  # BASELINE configs[4]'s perft(startpos, 7) under standard rules
+        note("fide7")
         f7 = fide_leg(eng, d, args, "perft(startpos, 7) RULES_FIDE", 7, ("startpos",), "fide_d7")
     if "fidesuite" in legs:  # BASELINE configs[2]: Kiwipete + the standard suite at depth 5
+        note("fidesuite")
         fs = fide_leg(eng, d, args, "Kiwipete + perft suite positions 3-6 + startpos at depth 5, RULES_FIDE", 5,
                       FIDE_SUITE, "fide_suite_d5")
 
@@ -860,16 +871,19 @@ def main():
     replay = None
     replay_host = None
     if "replay" in legs:
+        note("replay")
         replay, replay_host = replay_leg(eng, d, args)
 
     # ------------------------------------------- state hash
     shash = None
     if "hash" in legs:
+        note("hash")
         shash = state_hash_leg(eng, d, args)
 
     # ------------------------------------ transaction signatures
     txsig = None
     if "tx" in legs:
+        note("tx")
         txsig = txsig_leg(eng, d, args)
 
     v1 = validate_latency(eng) if "latency" in legs else None

@@ -106,6 +106,15 @@ def test_perft7_startpos_fide(engine):
     assert engine.perft(dchess.startpos(), 7, rules=FIDE)[0] == OG["perft_fide"]["startpos"]["perft"]["7"]
 
 
+@pytest.mark.parametrize("name,depth", [("startpos", 8), ("kiwipete", 6), ("pos3", 7), ("pos4", 6), ("pos6", 6)])
+def test_perft_fide_deep_published(engine, name, depth):
+    """FIDE past depth 7 and past the suite's depth 5, through the BFS levels
+    (startpos d8: ply 6 = 119M boards, 4.3 GB, then the final stage's two
+    plies): the published chessprogramming-wiki counts."""
+    e = OG["perft_fide"][name]
+    assert engine.perft(dchess.pos_from_fen(e["fen"]), depth, rules=FIDE)[0] == e["perft"][str(depth)]
+
+
 @pytest.mark.parametrize("depth,n_shards,split", [(6, 3, 4), (6, 2, 3)])
 def test_perft_startpos_fide_shards(engine, depth, n_shards, split):
     """FIDE through the same front end (k_make_count with FideRules, strided

@@ -35,7 +35,7 @@ if has pmc; then
   # 4 counter passes over every leg's kernels (one bench process per pass),
   # then per-kernel records -> $O/pmc_latest.json (tools/pmc_summary.py)
   rm -rf $O/pmc_p*
-  P="--steps 8 --warmup 1 --no-cpu --replay-steps 2 --hash-steps 1 --tx-steps 1 --only perft,perft8,perft9,replay,hash,tx"
+  P="--steps 4 --warmup 1 --no-cpu --replay-steps 2 --hash-steps 1 --tx-steps 1 --only perft,perft8,perft9,replay,hash,tx"
   pass() {  # $1 counters, $2 tag
     step "pmc $2"
     timeout -s KILL 240 rocprofv3 --pmc $1 --output-format csv -d $O/pmc_$2 -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err
@@ -57,7 +57,7 @@ if has fidepmc; then
   # key's per-dispatch average comes from one workload; merged into pmc_latest.json
   rm -rf $O/pmc_f*
   for leg in fide7 fidesuite; do
-    P="--steps 8 --warmup 1 --no-cpu --only $leg"
+    P="--steps 4 --warmup 1 --no-cpu --only $leg"
     fpass() { local c=$1 t=$2; step "pmc $t"; timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err; }
     fpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" f1$leg && \
     fpass "FETCH_SIZE" f2$leg && fpass "WRITE_SIZE" f3$leg && \
