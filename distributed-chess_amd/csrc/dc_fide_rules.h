@@ -35,6 +35,52 @@ __device__ __forceinline__ u64 king_attacks(u64 k) {
   return sh<8>(k) | sh<-8>(k) | sh<1>(k & kNotH) | sh<-1>(k & kNotA) | sh<9>(k & kNotH) | sh<7>(k & kNotA) |
          sh<-7>(k & kNotH) | sh<-9>(k & kNotA);
 }
+// TAB: king and knight attack sets from kAtt (one L1 load per piece instead
+// of eight shifts) -- the final stage's leaf counts only (k_count2b); the
+// single-workgroup top plies are latency-bound and keep the shifts
+#ifndef DC_FIDE_TAB_UNCOND
+#define DC_FIDE_TAB_UNCOND 0
+#endif
+#ifndef DC_FIDE_TAB_PARTS
+#define DC_FIDE_TAB_PARTS 7  // (diagnostics) 1 king sets, 2 enemy knight sets, 4 own knight counts
+#endif
+template <bool TAB>
+__device__ __forceinline__ u64 king_attacks_t(u64 k) {
+  if constexpr (TAB && (DC_FIDE_TAB_PARTS & 1)) {
+#if DC_FIDE_TAB_UNCOND == 1
+    // (diagnostics) the load issued by every lane, outside the branch
+    u64 t = kAtt.king[lsb(k | (1ull << 63)) & 63];
+    asm volatile("" : "+v"(t));
+    if ((k & (k - 1)) == 0) return k ? t : 0ull;
+#elif DC_FIDE_TAB_UNCOND == 2
+    // (diagnostics) the load waited for at once
+    if ((k & (k - 1)) == 0) {
+      u64 t = k ? kAtt.king[lsb(k) & 63] : 0ull;
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(t)::"memory");
+      return t;
+    }
+#elif DC_FIDE_TAB_UNCOND == 3
+    // (diagnostics) the table address in VGPRs (no SGPR base operand)
+    if ((k & (k - 1)) == 0) {
+      const u64* base = &kAtt.king[0];
+      asm volatile("" : "+v"(base));
+      return k ? base[lsb(k) & 63] : 0ull;
+    }
+#else
+    if ((k & (k - 1)) == 0) return k ? kAtt.king[lsb(k) & 63] : 0ull;
+#endif
+  }
+  return king_attacks(k);
+}
+template <bool TAB>
+__device__ __forceinline__ u64 knight_attacks_t(u64 n) {
+  if constexpr (TAB && (DC_FIDE_TAB_PARTS & 2)) {
+    u64 a = 0;
+    for (; n; n &= n - 1) a |= kAtt.knight[lsb(n) & 63];
+    return a;
+  }
+  return knight_attacks(n);
+}
 __device__ __forceinline__ u64 orth_attacks(u64 s, u64 empty) {
   return ray_attacks<8, kAll>(s, empty) | ray_attacks<-8, kAll>(s, empty) | ray_attacks<1, kNotA>(s, empty) |
          ray_attacks<-1, kNotH>(s, empty);
@@ -140,13 +186,13 @@ __device__ __forceinline__ void scan_dir(const FPos<STM>& f, int ksq, const Line
 #ifndef DC_FIDE_SNIPER
 #define DC_FIDE_SNIPER 1
 #endif
-template <int STM>
+template <int STM, bool TAB = false>
 __device__ __forceinline__ Analysis analyse(const FPos<STM>& f) {
   constexpr int THEM = 1 - STM;
   Analysis a;
   const u64 empty_nk = f.empty | f.K;
-  a.danger = pawn_attacks<THEM>(f.tP) | knight_attacks(f.tN) | king_attacks(f.tK) | orth_attacks(f.tO, empty_nk) |
-             diag_attacks(f.tD, empty_nk);
+  a.danger = pawn_attacks<THEM>(f.tP) | knight_attacks_t<TAB>(f.tN) | king_attacks_t<TAB>(f.tK) |
+             orth_attacks(f.tO, empty_nk) | diag_attacks(f.tD, empty_nk);
   a.checkers = 0;
   a.pinned = 0;
   a.ksq = f.K ? lsb(f.K) : -1;
@@ -238,14 +284,14 @@ __device__ __forceinline__ u64 castle_targets(const FPos<STM>& f, const Analysis
   return t;
 }
 
-// Number of legal moves (promotions count 4).
-template <int STM>
+// Number of legal moves (promotions count 4).  TAB: see king_attacks_t.
+template <int STM, bool TAB = false>
 __device__ __forceinline__ u32 fide_count(const Board& b, u32 meta) {
   typedef FDir<STM> FD;
   const FPos<STM> f = fpos<STM>(b);
-  const Analysis a = analyse<STM>(f);
+  const Analysis a = analyse<STM, TAB>(f);
   const u64 notus = ~f.us;
-  u32 c = pc(king_attacks(f.K) & notus & ~a.danger);
+  u32 c = pc(king_attacks_t<TAB>(f.K) & notus & ~a.danger);
   if (a.checkers & (a.checkers - 1)) return c;  // double check: king moves only
   const u64 tm = notus & a.cmask;
   // free (unpinned) pieces, one popcount per direction class
@@ -257,9 +303,13 @@ __device__ __forceinline__ u32 fide_count(const Board& b, u32 meta) {
   const u64 ce = sh<FD::CE>(Pf & kNotH) & f.them & a.cmask;
   c += pc(p1) + pc(push2) + pc(cw) + pc(ce) + 3 * (pc(p1 & FD::LAST) + pc(cw & FD::LAST) + pc(ce & FD::LAST));
   const u64 n = f.N & ~a.pinned;
-  c += pc(sh<17>(n & kNotH) & tm) + pc(sh<15>(n & kNotA) & tm) + pc(sh<10>(n & kNotGH) & tm) +
-       pc(sh<6>(n & kNotAB) & tm) + pc(sh<-6>(n & kNotGH) & tm) + pc(sh<-10>(n & kNotAB) & tm) +
-       pc(sh<-15>(n & kNotH) & tm) + pc(sh<-17>(n & kNotA) & tm);
+  if constexpr (TAB && (DC_FIDE_TAB_PARTS & 4)) {
+    for (u64 k = n; k; k &= k - 1) c += pc(kAtt.knight[lsb(k) & 63] & tm);
+  } else {
+    c += pc(sh<17>(n & kNotH) & tm) + pc(sh<15>(n & kNotA) & tm) + pc(sh<10>(n & kNotGH) & tm) +
+         pc(sh<6>(n & kNotAB) & tm) + pc(sh<-6>(n & kNotGH) & tm) + pc(sh<-10>(n & kNotAB) & tm) +
+         pc(sh<-15>(n & kNotH) & tm) + pc(sh<-17>(n & kNotA) & tm);
+  }
   const u64 e = f.empty, O = f.O & ~a.pinned, D = f.D & ~a.pinned;
   c += pc(ray_attacks<8, kAll>(O, e) & tm) + pc(ray_attacks<-8, kAll>(O, e) & tm) +
        pc(ray_attacks<1, kNotA>(O, e) & tm) + pc(ray_attacks<-1, kNotH>(O, e) & tm);

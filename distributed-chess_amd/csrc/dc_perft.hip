@@ -47,6 +47,8 @@ struct RefRules {
   static constexpr int kTopThreads = 1024;    // k_expand_top's one workgroup
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32) { return ref_count<STM>(b); }
+  template <int STM>
+  __device__ static __forceinline__ u32 count_final(const Board& b, u32) { return ref_count<STM>(b); }
   template <int STM, class V>
   __device__ static __forceinline__ void for_each(const Board& b, u32, V&& v) {
     ref_for_each_move<STM>(b, [&](int f, int t) { v(f, t, 0); });
@@ -58,6 +60,9 @@ struct RefRules {
   }
 };
 
+#ifndef DC_FIDE_TAB
+#define DC_FIDE_TAB 0  // 1: k_count2b<FideRules> leaf counts with kAtt king/knight sets -- WRONG counts, see DESIGN.md §3.6
+#endif
 #ifndef DC_FIDE_MINB
 #define DC_FIDE_MINB 2  // (A/B: 4 = the round-3 budget, 128 VGPRs with spills)
 #endif
@@ -72,6 +77,11 @@ struct FideRules {
   static constexpr int kTopThreads = 512;
   template <int STM>
   __device__ static __forceinline__ u32 count(const Board& b, u32 meta) { return fide_count<STM>(b, meta); }
+  // the final stage's leaf counts: king/knight attack sets from kAtt
+  template <int STM>
+  __device__ static __forceinline__ u32 count_final(const Board& b, u32 meta) {
+    return fide_count<STM, DC_FIDE_TAB != 0>(b, meta);
+  }
   template <int STM, class V>
   __device__ static __forceinline__ void for_each(const Board& b, u32 meta, V&& v) {
     fide_for_each_move<STM>(b, meta, v);
@@ -973,7 +983,7 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
           Board ch = sh.par[pl];
           const u32 cm = R::template make<STM>(ch, R::kMeta ? sh.pmeta[pl] : 0u, (int)(e & 63), (int)((e >> 6) & 63),
                                                (int)((e >> 12) & 7));
-          const u32 k = R::template count<1 - STM>(ch, cm);
+          const u32 k = R::template count_final<1 - STM>(ch, cm);
           const u32 ptag = sh.ptag[pl];
           if (ptag == tag0) acc += k;
           else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
