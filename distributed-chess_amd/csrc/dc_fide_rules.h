@@ -201,7 +201,25 @@ __device__ __forceinline__ Analysis analyse(const FPos<STM>& f) {
   a.checkers = (pawn_attacks<STM>(f.K) & f.tP) | (knight_attacks(f.K) & f.tN);
   const Lines l = lines_of(a.ksq);
   u64 chk = a.checkers, pin = 0;
-#if DC_FIDE_SNIPER
+#if DC_FIDE_SNIPER == 2
+  // (diagnostics) the same gate as a per-lane branch (no __ballot)
+  if ((l.file & f.tO) != 0) {
+    scan_dir<STM, 0>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 1>(f, a.ksq, l, chk, pin);
+  }
+  if ((l.rank & f.tO) != 0) {
+    scan_dir<STM, 2>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 3>(f, a.ksq, l, chk, pin);
+  }
+  if ((l.diag & f.tD) != 0) {
+    scan_dir<STM, 4>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 5>(f, a.ksq, l, chk, pin);
+  }
+  if ((l.anti & f.tD) != 0) {
+    scan_dir<STM, 6>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 7>(f, a.ksq, l, chk, pin);
+  }
+#elif DC_FIDE_SNIPER
   // a line through the king with no enemy slider of its kind on it can hold
   // neither a slider check nor a pin: a wave none of whose lanes has one
   // skips that line's two scans (round 4: the eight scans were ~19 % of the
