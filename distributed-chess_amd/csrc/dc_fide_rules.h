@@ -471,6 +471,242 @@ __device__ __forceinline__ void fide_for_each_move(const Board& b, u32 meta, Vis
   }
 }
 
+// ------------------------------------------- simple children (final stage)
+// For a parent P (side STM to move, opponent THEM), a legal STM move f -> t is
+// *simple* when it is quiet (t empty; no promotion, castling, en passant or
+// double push), STM is not in check, and neither square is in a set where a
+// change of occupancy or of STM's attacks could change THEM's legal moves:
+//   all      THEM's king zone Z' (king, neighbours, back-rank castling squares
+//            while THEM has a right), THEM's slider rays and pawn push /
+//            double-push / capture squares, the squares between Z' and an STM
+//            slider attacking it, and the pin segments from THEM's king (king
+//            -> THEM piece -> up to the next piece)
+//   fsrc     (f only) a first piece seen from Z' with an STM slider of the
+//            line's kind behind it (moving it uncovers an attack)
+//   t_orth / t_diag  (t only, rook/queen and bishop/queen movers) the open
+//            lines of sight from Z'
+//   lk/ln/lp (king/knight/pawn movers) squares from which such a piece hits Z'
+// The child's THEM count then equals c0 = THEM's legal moves in P with THEM
+// to move and no en-passant square.  Pinned with the oracle on random
+// descendants of the published suite positions (tools/fide_simple_proto.py:
+// 0 mismatches, 47 % of the children of startpos ply-5 parents simple);
+// the GPU tests pin the kernel through the published perft tables.
+struct Sens {
+  u64 all, fsrc, t_orth, t_diag, lk, ln, lp;
+};
+
+template <int S, u64 M, int SO, u64 MO>
+__device__ __forceinline__ void sens_dir(u64 zp, u64 e_nk, u64 occ_nk, u64 st, u64& all, u64& fsrc, u64& tt) {
+  const u64 fd = ray_attacks<S, M>(zp, e_nk);   // seen from Z' toward S (first piece included)
+  const u64 rd = ray_attacks<SO, MO>(st, e_nk);  // STM sliders of the kind, looking back
+  const u64 b1 = fd & occ_nk;
+  tt |= fd & e_nk;
+  all |= (fd & rd & e_nk) | (b1 & st);
+  fsrc |= b1 & rd;
+}
+
+// From THEM's king along direction D (scan_dir's numbering): when the first
+// piece is THEM's, the squares up to and including the second piece (the
+// first excluded): a change there can make or break a pin.
+template <int D>
+__device__ __forceinline__ u64 pin_seg(const Lines& l, int ksq, u64 occ, u64 them) {
+  constexpr bool UP = (D & 1) == 0;
+  const u64 line = (D < 2) ? l.file : (D < 4) ? l.rank : (D < 6) ? l.diag : l.anti;
+  const u64 ray = line & (UP ? above_mask(ksq) : below_mask(ksq));
+  const u64 blk = occ & ray;
+  const u64 m1 = UP ? (blk & (0ull - blk)) : (blk ? (1ull << msb(blk)) : 0ull);
+  const u64 rest = blk & ~m1;
+  const u64 m2 = UP ? (rest & (0ull - rest)) : (rest ? (1ull << msb(rest)) : 0ull);
+  const u64 upto = UP ? (m2 ? ((m2 << 1) - 1) : ~0ull) : (m2 ? ~(m2 - 1) : ~0ull);  // m2 = bit 63: (0 - 1) = all
+  return (m1 & them) ? (ray & upto & ~m1) : 0ull;
+}
+
+template <int STM>
+__device__ __forceinline__ Sens fide_sens(const Board& b, u32 meta) {
+  constexpr int THEM = 1 - STM;
+  typedef FDir<THEM> TD;
+  const FPos<STM> f = fpos<STM>(b);
+  Sens s{~0ull, 0, 0, 0, 0, 0, 0};  // all = every square: no child simple
+  if (!f.tK || (f.tK & (f.tK - 1)) || !f.K || (f.K & (f.K - 1))) return s;
+  const u64 ro = orth_attacks(f.tO, f.empty) | diag_attacks(f.tD, f.empty);
+  if ((ro & f.K) || (pawn_attacks<STM>(f.K) & f.tP) || (knight_attacks(f.K) & f.tN)) return s;  // STM in check
+  const u64 push = sh<TD::F>(f.tP);
+  const u32 rights = meta & (THEM ? (CR_BK | CR_BQ) : (CR_WK | CR_WQ));
+  const u64 zp = f.tK | king_attacks(f.tK) | (rights ? (THEM ? (0x7Eull << 56) : 0x7Eull) : 0ull);
+  u64 all = ro | push | sh<TD::F>(push & TD::ROW_AFTER1) | pawn_attacks<THEM>(f.tP) | zp;
+  const u64 occ_nk = f.occ & ~f.tK, e_nk = ~occ_nk;
+  u64 fsrc = 0, to = 0, td = 0;
+  sens_dir<8, kAll, -8, kAll>(zp, e_nk, occ_nk, f.O, all, fsrc, to);
+  sens_dir<-8, kAll, 8, kAll>(zp, e_nk, occ_nk, f.O, all, fsrc, to);
+  sens_dir<1, kNotA, -1, kNotH>(zp, e_nk, occ_nk, f.O, all, fsrc, to);
+  sens_dir<-1, kNotH, 1, kNotA>(zp, e_nk, occ_nk, f.O, all, fsrc, to);
+  sens_dir<9, kNotA, -9, kNotH>(zp, e_nk, occ_nk, f.D, all, fsrc, td);
+  sens_dir<-9, kNotH, 9, kNotA>(zp, e_nk, occ_nk, f.D, all, fsrc, td);
+  sens_dir<7, kNotH, -7, kNotA>(zp, e_nk, occ_nk, f.D, all, fsrc, td);
+  sens_dir<-7, kNotA, 7, kNotH>(zp, e_nk, occ_nk, f.D, all, fsrc, td);
+  const int ksq = lsb(f.tK);
+  const Lines l = lines_of(ksq);
+  all |= pin_seg<0>(l, ksq, f.occ, f.them) | pin_seg<1>(l, ksq, f.occ, f.them) | pin_seg<2>(l, ksq, f.occ, f.them) |
+         pin_seg<3>(l, ksq, f.occ, f.them) | pin_seg<4>(l, ksq, f.occ, f.them) | pin_seg<5>(l, ksq, f.occ, f.them) |
+         pin_seg<6>(l, ksq, f.occ, f.them) | pin_seg<7>(l, ksq, f.occ, f.them);
+  s.all = all;
+  s.fsrc = fsrc;
+  s.t_orth = to;
+  s.t_diag = td;
+  s.lk = king_attacks(zp);
+  s.ln = knight_attacks(zp);
+  s.lp = pawn_attacks<THEM>(zp);  // an STM pawn there attacks Z'
+  return s;
+}
+
+// fide_for_each_move restricted to the children that are not simple (same
+// order as fide_for_each_move with the simple ones left out); returns the
+// number of simple children.  `sn(k)` reads one of the sets below, made by
+// sens_masks from a Sens: the final stage keeps them in LDS and reads them
+// where they are used, so they hold no registers across the enumeration loops.
+enum : int {
+  SN_ALL = 0,  // all
+  SN_SRC,      // all | fsrc (f of any mover)
+  SN_TORTH,    // all | t_orth (t of a rook/queen mover)
+  SN_TDIAG,    // all | t_diag (t of a bishop/queen mover)
+  SN_LK, SN_LN, SN_LP,
+  SN_COUNT
+};
+__device__ __forceinline__ void sens_masks(const Sens& s, u64 (&m)[SN_COUNT]) {
+  m[SN_ALL] = s.all;
+  m[SN_SRC] = s.all | s.fsrc;
+  m[SN_TORTH] = s.all | s.t_orth;
+  m[SN_TDIAG] = s.all | s.t_diag;
+  m[SN_LK] = s.lk;
+  m[SN_LN] = s.ln;
+  m[SN_LP] = s.lp;
+}
+template <int STM, class SensAt, class Visit>
+__device__ __forceinline__ u32 fide_for_each_split(const Board& b, u32 meta, SensAt&& sn, Visit&& visit) {
+  typedef FDir<STM> FD;
+  const FPos<STM> f = fpos<STM>(b);
+  const Analysis a = analyse<STM>(f);
+  const u64 notus = ~f.us;
+  u32 ns = 0;
+  auto emit = [&](int from, u64 targets) {
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(from, t, 0);
+    }
+  };
+  auto emit_pawn = [&](u64 targets, int delta) {
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      if ((1ull << t) & FD::LAST) {
+        for (int pr = 1; pr <= 4; ++pr) visit(t - delta, t, pr);
+      } else {
+        visit(t - delta, t, 0);
+      }
+    }
+  };
+  if (a.ksq >= 0) {
+    const u64 kt = king_attacks(f.K) & notus & ~a.danger;
+    const u64 ks = (f.K & (sn(SN_SRC) | sn(SN_LK))) ? 0ull : and_andn(kt, f.empty, sn(SN_ALL) | sn(SN_LK));
+    ns += pc(ks);
+    emit(a.ksq, (kt & ~ks) | castle_targets<STM>(f, a, meta, b));
+  }
+  if (a.checkers & (a.checkers - 1)) return ns;
+  const u64 tm = notus & a.cmask;
+  const u64 Pf = f.P & ~a.pinned;
+  const u64 push1 = sh<FD::F>(Pf) & f.empty;
+  // (in check, the `all` set is every square: nothing below is simple)
+  const u64 ps = sh<FD::F>(Pf & ~(sn(SN_SRC) | sn(SN_LP))) & f.empty & ~(sn(SN_ALL) | sn(SN_LP) | FD::LAST);
+  ns += pc(ps);
+  emit_pawn((push1 & a.cmask) & ~ps, FD::F);
+  emit_pawn(sh<FD::F>(push1 & FD::ROW_AFTER1) & f.empty & a.cmask, 2 * FD::F);
+  emit_pawn(sh<FD::CW>(Pf & kNotA) & f.them & a.cmask, FD::CW);
+  emit_pawn(sh<FD::CE>(Pf & kNotH) & f.them & a.cmask, FD::CE);
+  const u64 n = f.N & ~a.pinned;
+  const u64 nsrc = n & ~(sn(SN_SRC) | sn(SN_LN)), nt = f.empty & ~(sn(SN_ALL) | sn(SN_LN));
+  auto leap = [&](u64 targets, u64 simple, int delta) {
+    ns += pc(simple);
+    targets &= ~simple;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      visit(t - delta, t, 0);
+    }
+  };
+  leap(sh<17>(n & kNotH) & tm, sh<17>(nsrc & kNotH) & nt, 17);
+  leap(sh<15>(n & kNotA) & tm, sh<15>(nsrc & kNotA) & nt, 15);
+  leap(sh<10>(n & kNotGH) & tm, sh<10>(nsrc & kNotGH) & nt, 10);
+  leap(sh<6>(n & kNotAB) & tm, sh<6>(nsrc & kNotAB) & nt, 6);
+  leap(sh<-6>(n & kNotGH) & tm, sh<-6>(nsrc & kNotGH) & nt, -6);
+  leap(sh<-10>(n & kNotAB) & tm, sh<-10>(nsrc & kNotAB) & nt, -10);
+  leap(sh<-15>(n & kNotH) & tm, sh<-15>(nsrc & kNotH) & nt, -15);
+  leap(sh<-17>(n & kNotA) & tm, sh<-17>(nsrc & kNotA) & nt, -17);
+  const u64 e = f.empty, O = f.O & ~a.pinned, D = f.D & ~a.pinned;
+  auto slide = [&](u64 targets, auto dtag) {
+    constexpr int DD = decltype(dtag)::value;
+    while (targets) {
+      const int t = lsb(targets);
+      targets &= targets - 1;
+      const int src = slider_source<DD, false>(f.occ, t);
+      // a rook/bishop mover is tested against its own line kind, a queen
+      // against both; captures are never simple
+      const bool q = ((f.O & f.D) >> src) & 1;
+      u32 bad = (u32)(f.occ >> t) | (u32)(sn(SN_SRC) >> src) | (u32)(sn(DD < 4 ? SN_TORTH : SN_TDIAG) >> t);
+      if (q) bad |= (u32)(sn(DD < 4 ? SN_TDIAG : SN_TORTH) >> t);
+      // ns updated unconditionally: `else ++ns` let the compiler merge the two
+      // counter updates of the counting pass (the visitor's and ns) into one
+      // through a selected address, which kept both in scratch memory
+      ns += (bad & 1) ^ 1u;
+      if (bad & 1) visit(src, t, 0);
+    }
+  };
+  slide(ray_attacks<8, kAll>(O, e) & tm, std::integral_constant<int, 0>{});
+  slide(ray_attacks<-8, kAll>(O, e) & tm, std::integral_constant<int, 1>{});
+  slide(ray_attacks<1, kNotA>(O, e) & tm, std::integral_constant<int, 2>{});
+  slide(ray_attacks<-1, kNotH>(O, e) & tm, std::integral_constant<int, 3>{});
+  slide(ray_attacks<9, kNotA>(D, e) & tm, std::integral_constant<int, 4>{});
+  slide(ray_attacks<-9, kNotH>(D, e) & tm, std::integral_constant<int, 5>{});
+  slide(ray_attacks<7, kNotH>(D, e) & tm, std::integral_constant<int, 6>{});
+  slide(ray_attacks<-7, kNotA>(D, e) & tm, std::integral_constant<int, 7>{});
+  if (!a.checkers) {
+    u64 pins = a.pinned;
+    while (pins) {
+      const int s = lsb(pins);
+      pins &= pins - 1;
+      const u64 line = line_through(a.ksq, s);
+      const u64 bit = 1ull << s;
+      if (bit & f.P) {
+        const u64 q1 = sh<FD::F>(bit) & f.empty;
+        u64 t = (q1 | (sh<FD::F>(q1 & FD::ROW_AFTER1) & f.empty) | (pawn_attacks<STM>(bit) & f.them)) & line;
+        while (t) {
+          const int to = lsb(t);
+          t &= t - 1;
+          if ((1ull << to) & FD::LAST) {
+            for (int pr = 1; pr <= 4; ++pr) visit(s, to, pr);
+          } else {
+            visit(s, to, 0);
+          }
+        }
+      } else if (bit & (f.O | f.D)) {
+        const Lines ls = lines_of(s);
+        const bool orth_line = (line == ls.file) || (line == ls.rank);
+        if ((orth_line && (bit & f.O)) || (!orth_line && (bit & f.D))) emit(s, line_attacks(s, line, f.occ) & notus);
+      }
+    }
+  }
+  const int ep = meta_ep(meta);
+  if (ep >= 0) {
+    u64 cand = pawn_attacks<1 - STM>(1ull << ep) & f.P;
+    while (cand) {
+      const int s = lsb(cand);
+      cand &= cand - 1;
+      if (ep_legal<STM>(f, a.ksq, s, ep, ep - FD::F)) visit(s, ep, 0);
+    }
+  }
+  return ns;
+}
+
 // Promotion piece -> kind code (1 N, 2 B, 3 R, 4 Q).
 __device__ __forceinline__ u32 promo_code(int promo) {
   return promo == 1 ? KC_N : promo == 2 ? KC_B : promo == 3 ? KC_R : KC_Q;

@@ -40,6 +40,7 @@ namespace dc {
 // ------------------------------------------------------------ rules policies
 struct RefRules {
   static constexpr bool kMeta = false;
+  static constexpr bool kSplit = false;  // k_count2b: REF's final stage split is k_count2c / k_count3c
   // blocks of 256 per CU the level / final-stage kernels are built for
   // (FIDE's legal-move analysis needs the registers of 2: spill-free)
   static constexpr int kMinBlocks = 4;
@@ -66,8 +67,12 @@ struct RefRules {
 #ifndef DC_FIDE_MINB
 #define DC_FIDE_MINB 2  // (A/B: 4 = the round-3 budget, 128 VGPRs with spills)
 #endif
+#ifndef DC_FIDE_SPLIT
+#define DC_FIDE_SPLIT 1  // k_count2b<FideRules>: simple children counted as c0 (fide_sens); 0: every child made
+#endif
 struct FideRules {
   static constexpr bool kMeta = true;
+  static constexpr bool kSplit = DC_FIDE_SPLIT != 0;
   static constexpr int kMinBlocks = DC_FIDE_MINB;
   // k_count2b: 3 blocks/CU (148 VGPRs, 0 B) since the parent is re-read from
   // LDS for the enumeration (its registers are free across the child loop)
@@ -917,24 +922,36 @@ __global__ __launch_bounds__(256, 4) void k_count2(const Board* __restrict__ nod
 // all 256 lanes take one child per round: make it, bulk-count its moves.  The
 // work unit is a 256-parent chunk, so even a ~200k-node final level (perft 6)
 // spreads evenly over the GPU, and no child ever round-trips through HBM.
-constexpr u32 kC2bCap = 256 * 28;  // child slots per window (4 blocks per CU)
+// FIDE (kSplit): the parents' simple children (fide_sens, dc_fide_rules.h)
+// are never made: each adds c0, the opponent's count in the parent; only the
+// others take slots, whose area shrinks to make room for the per-parent
+// sensitivity sets (three blocks per CU either way).
+template <bool SPLIT>
+struct C2bCfg {
+  static constexpr u32 kCap = SPLIT ? 256 * 22 : 256 * 28;  // child slots per window
+};
 
+template <bool SPLIT>
 struct C2bShared {
   Board par[256];
   u32 pmeta[256];
-  u32 slot[kC2bCap];
+  u32 slot[C2bCfg<SPLIT>::kCap];
   u64 hist[256];
   u64 wsum[4];
   uint16_t ptag[256];
+  u64 sens[SPLIT ? SN_COUNT : 1][256];  // sens_masks, [set][parent]
 };
 
 template <class R, int STM>
 __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
                                                     u64* __restrict__ divide) {
-  __shared__ C2bShared sh;
+  constexpr bool SPLIT = R::kSplit;
+  constexpr u32 kC2bCap = C2bCfg<SPLIT>::kCap;
+  __shared__ C2bShared<SPLIT> sh;
   tag_hist_init(sh.hist);
   const u32 tid = threadIdx.x;
+  const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // Equal contiguous share of the level per resident block (the grid is one
   // resident wave of blocks, so every CU carries the same number of parents).
   const u64 lo = rng->lo, hi = rng->hi;
@@ -950,7 +967,23 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
       pm = load_meta<R>(meta, i);
       tag = tags[i];
     }
-    const u32 cnt = valid ? R::template count<STM>(p, pm) : 0;
+    u32 cnt = 0;
+    u64 simple_leaves = 0;  // simple children x c0 (SPLIT)
+    // the lane's sensitivity sets, read from LDS where the enumeration uses
+    // them (the thread index rebuilt at each use, otid: no address kept live)
+    auto sens_at = [&](int k) -> u64 { return sh.sens[k][otid(wave)]; };
+    if constexpr (SPLIT) {
+      if (valid) {
+        u64 m[SN_COUNT];
+        sens_masks(fide_sens<STM>(p, pm), m);
+#pragma unroll
+        for (int k = 0; k < SN_COUNT; ++k) sh.sens[k][tid] = m[k];
+        const u32 ns = fide_for_each_split<STM>(p, pm, sens_at, [&](int, int, int) { ++cnt; });
+        if (ns) simple_leaves = (u64)ns * fide_count<1 - STM>(p, pm & 15u);  // THEM to move, no en passant
+      }
+    } else {
+      cnt = valid ? R::template count<STM>(p, pm) : 0;
+    }
     u64 total64;
     const u32 excl = (u32)block_excl_scan64<4>(cnt, sh.wsum, &total64);
     const u32 total = (u32)total64;
@@ -960,6 +993,10 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
     __syncthreads();
     const u32 tag0 = sh.ptag[0];
     u64 acc = 0;  // grandchildren under parents whose tag == tag0 (the norm: nodes stay ordered by root)
+    if constexpr (SPLIT) {
+      if (tag == tag0) acc = simple_leaves;
+      else if (simple_leaves) atomicAdd((unsigned long long*)&sh.hist[tag], (unsigned long long)simple_leaves);
+    }
     for (u32 base = 0; base < total; base += kC2bCap) {
       if (base) __syncthreads();  // previous window fully read
       u32 j = excl;
@@ -968,10 +1005,16 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
         // child loop (FIDE fits 4 blocks/CU only with every such VGPR freed)
         const Board pp = sh.par[tid];
         const u32 ppm = R::kMeta ? sh.pmeta[tid] : 0u;
-        R::template for_each<STM>(pp, ppm, [&](int f, int t, int promo) {
-          if (j >= base && j - base < kC2bCap) sh.slot[j - base] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | (tid << 15);
+        j -= base;  // slot index in this window (wraps below 0 for earlier windows)
+        auto put = [&](int f, int t, int promo) {
+          if (j < kC2bCap) sh.slot[j] = (u32)f | ((u32)t << 6) | ((u32)promo << 12) | ((SPLIT ? otid(wave) : tid) << 15);
           ++j;
-        });
+        };
+        if constexpr (SPLIT) {
+          (void)fide_for_each_split<STM>(pp, ppm, sens_at, put);
+        } else {
+          R::template for_each<STM>(pp, ppm, put);
+        }
       }
       __syncthreads();
       const u32 nslots = min(kC2bCap, total - base);
