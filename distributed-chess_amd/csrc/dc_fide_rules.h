@@ -482,7 +482,9 @@ __device__ __forceinline__ void fide_for_each_move(const Board& b, u32 meta, Vis
 //            slider attacking it, and the pin segments from THEM's king (king
 //            -> THEM piece -> up to the next piece)
 //   fsrc     (f only) a first piece seen from Z' with an STM slider of the
-//            line's kind behind it (moving it uncovers an attack)
+//            line's kind behind it (moving it uncovers an attack), and an STM
+//            piece first on a line from THEM's king with a THEM piece second
+//            (moving it can pin that piece)
 //   t_orth / t_diag  (t only, rook/queen and bishop/queen movers) the open
 //            lines of sight from Z'
 //   lk/ln/lp (king/knight/pawn movers) squares from which such a piece hits Z'
@@ -507,9 +509,11 @@ __device__ __forceinline__ void sens_dir(u64 zp, u64 e_nk, u64 occ_nk, u64 st, u
 
 // From THEM's king along direction D (scan_dir's numbering): when the first
 // piece is THEM's, the squares up to and including the second piece (the
-// first excluded): a change there can make or break a pin.
+// first excluded): a change there can make or break a pin.  When the first
+// piece is STM's and the second THEM's, moving the first can pin the second
+// (a slider behind it): the first goes into fsrc.
 template <int D>
-__device__ __forceinline__ u64 pin_seg(const Lines& l, int ksq, u64 occ, u64 them) {
+__device__ __forceinline__ u64 pin_seg(const Lines& l, int ksq, u64 occ, u64 them, u64& fsrc) {
   constexpr bool UP = (D & 1) == 0;
   const u64 line = (D < 2) ? l.file : (D < 4) ? l.rank : (D < 6) ? l.diag : l.anti;
   const u64 ray = line & (UP ? above_mask(ksq) : below_mask(ksq));
@@ -518,6 +522,7 @@ __device__ __forceinline__ u64 pin_seg(const Lines& l, int ksq, u64 occ, u64 the
   const u64 rest = blk & ~m1;
   const u64 m2 = UP ? (rest & (0ull - rest)) : (rest ? (1ull << msb(rest)) : 0ull);
   const u64 upto = UP ? (m2 ? ((m2 << 1) - 1) : ~0ull) : (m2 ? ~(m2 - 1) : ~0ull);  // m2 = bit 63: (0 - 1) = all
+  fsrc |= (m2 & them) ? (m1 & ~them) : 0ull;
   return (m1 & them) ? (ray & upto & ~m1) : 0ull;
 }
 
@@ -546,9 +551,10 @@ __device__ __forceinline__ Sens fide_sens(const Board& b, u32 meta) {
   sens_dir<-7, kNotA, 7, kNotH>(zp, e_nk, occ_nk, f.D, all, fsrc, td);
   const int ksq = lsb(f.tK);
   const Lines l = lines_of(ksq);
-  all |= pin_seg<0>(l, ksq, f.occ, f.them) | pin_seg<1>(l, ksq, f.occ, f.them) | pin_seg<2>(l, ksq, f.occ, f.them) |
-         pin_seg<3>(l, ksq, f.occ, f.them) | pin_seg<4>(l, ksq, f.occ, f.them) | pin_seg<5>(l, ksq, f.occ, f.them) |
-         pin_seg<6>(l, ksq, f.occ, f.them) | pin_seg<7>(l, ksq, f.occ, f.them);
+  all |= pin_seg<0>(l, ksq, f.occ, f.them, fsrc) | pin_seg<1>(l, ksq, f.occ, f.them, fsrc) |
+         pin_seg<2>(l, ksq, f.occ, f.them, fsrc) | pin_seg<3>(l, ksq, f.occ, f.them, fsrc) |
+         pin_seg<4>(l, ksq, f.occ, f.them, fsrc) | pin_seg<5>(l, ksq, f.occ, f.them, fsrc) |
+         pin_seg<6>(l, ksq, f.occ, f.them, fsrc) | pin_seg<7>(l, ksq, f.occ, f.them, fsrc);
   s.all = all;
   s.fsrc = fsrc;
   s.t_orth = to;
@@ -705,6 +711,101 @@ __device__ __forceinline__ u32 fide_for_each_split(const Board& b, u32 meta, Sen
     }
   }
   return ns;
+}
+
+// The counting pass of the split without enumerating: fide_for_each_split's
+// visits (returned) and its simple children (ns), set-wise -- the same
+// classification, so the slot offsets it yields match the enumeration that
+// fills them.  Sliders: the targets of sources off SN_SRC come from fills of
+// those sources alone (the others still block: they stay occupied), rooks and
+// bishops tested against their line kind's target set, queens against both.
+template <int STM, class SensAt>
+__device__ __forceinline__ u32 fide_count_split(const Board& b, u32 meta, SensAt&& sn, u32& ns_out) {
+  typedef FDir<STM> FD;
+  const FPos<STM> f = fpos<STM>(b);
+  const Analysis a = analyse<STM>(f);
+  const u64 notus = ~f.us;
+  u32 c = 0, ns = 0;
+  if (a.ksq >= 0) {
+    const u64 kt = king_attacks(f.K) & notus & ~a.danger;
+    const u64 ks = (f.K & (sn(SN_SRC) | sn(SN_LK))) ? 0ull : and_andn(kt, f.empty, sn(SN_ALL) | sn(SN_LK));
+    ns += pc(ks);
+    c += pc(kt & ~ks) + pc(castle_targets<STM>(f, a, meta, b));
+  }
+  if (a.checkers & (a.checkers - 1)) {
+    ns_out = ns;
+    return c;
+  }
+  const u64 tm = notus & a.cmask;
+  const u64 Pf = f.P & ~a.pinned;
+  const u64 push1 = sh<FD::F>(Pf) & f.empty;
+  const u64 ps = sh<FD::F>(Pf & ~(sn(SN_SRC) | sn(SN_LP))) & f.empty & ~(sn(SN_ALL) | sn(SN_LP) | FD::LAST);
+  const u64 p1 = push1 & a.cmask & ~ps;
+  const u64 push2 = sh<FD::F>(push1 & FD::ROW_AFTER1) & f.empty & a.cmask;
+  const u64 cw = sh<FD::CW>(Pf & kNotA) & f.them & a.cmask;
+  const u64 ce = sh<FD::CE>(Pf & kNotH) & f.them & a.cmask;
+  ns += pc(ps);
+  c += pc(p1) + pc(push2) + pc(cw) + pc(ce) + 3 * (pc(p1 & FD::LAST) + pc(cw & FD::LAST) + pc(ce & FD::LAST));
+  const u64 n = f.N & ~a.pinned;
+  const u64 nsrc = n & ~(sn(SN_SRC) | sn(SN_LN)), nt = f.empty & ~(sn(SN_ALL) | sn(SN_LN));
+  auto leap = [&](u64 targets, u64 simple) {
+    ns += pc(simple);
+    c += pc(targets & ~simple);
+  };
+  leap(sh<17>(n & kNotH) & tm, sh<17>(nsrc & kNotH) & nt);
+  leap(sh<15>(n & kNotA) & tm, sh<15>(nsrc & kNotA) & nt);
+  leap(sh<10>(n & kNotGH) & tm, sh<10>(nsrc & kNotGH) & nt);
+  leap(sh<6>(n & kNotAB) & tm, sh<6>(nsrc & kNotAB) & nt);
+  leap(sh<-6>(n & kNotGH) & tm, sh<-6>(nsrc & kNotGH) & nt);
+  leap(sh<-10>(n & kNotAB) & tm, sh<-10>(nsrc & kNotAB) & nt);
+  leap(sh<-15>(n & kNotH) & tm, sh<-15>(nsrc & kNotH) & nt);
+  leap(sh<-17>(n & kNotA) & tm, sh<-17>(nsrc & kNotA) & nt);
+  const u64 e = f.empty, O = f.O & ~a.pinned, D = f.D & ~a.pinned;
+  const u64 q = O & D, qs = q & ~sn(SN_SRC);
+  const u64 rs = O & ~q & ~sn(SN_SRC), bs = D & ~q & ~sn(SN_SRC);
+  const u64 qt = ~(sn(SN_TORTH) | sn(SN_TDIAG)) & e;
+  const u64 ot = ~sn(SN_TORTH) & e, dt = ~sn(SN_TDIAG) & e;
+  auto slide = [&](u64 all_t, u64 simple) {
+    ns += pc(simple);
+    c += pc(all_t & ~simple);
+  };
+  slide(ray_attacks<8, kAll>(O, e) & tm, (ray_attacks<8, kAll>(rs, e) & ot) | (ray_attacks<8, kAll>(qs, e) & qt));
+  slide(ray_attacks<-8, kAll>(O, e) & tm, (ray_attacks<-8, kAll>(rs, e) & ot) | (ray_attacks<-8, kAll>(qs, e) & qt));
+  slide(ray_attacks<1, kNotA>(O, e) & tm, (ray_attacks<1, kNotA>(rs, e) & ot) | (ray_attacks<1, kNotA>(qs, e) & qt));
+  slide(ray_attacks<-1, kNotH>(O, e) & tm, (ray_attacks<-1, kNotH>(rs, e) & ot) | (ray_attacks<-1, kNotH>(qs, e) & qt));
+  slide(ray_attacks<9, kNotA>(D, e) & tm, (ray_attacks<9, kNotA>(bs, e) & dt) | (ray_attacks<9, kNotA>(qs, e) & qt));
+  slide(ray_attacks<-9, kNotH>(D, e) & tm, (ray_attacks<-9, kNotH>(bs, e) & dt) | (ray_attacks<-9, kNotH>(qs, e) & qt));
+  slide(ray_attacks<7, kNotH>(D, e) & tm, (ray_attacks<7, kNotH>(bs, e) & dt) | (ray_attacks<7, kNotH>(qs, e) & qt));
+  slide(ray_attacks<-7, kNotA>(D, e) & tm, (ray_attacks<-7, kNotA>(bs, e) & dt) | (ray_attacks<-7, kNotA>(qs, e) & qt));
+  if (!a.checkers) {
+    u64 pins = a.pinned;
+    while (pins) {
+      const int s = lsb(pins);
+      pins &= pins - 1;
+      const u64 line = line_through(a.ksq, s);
+      const u64 bit = 1ull << s;
+      if (bit & f.P) {
+        const u64 q1 = sh<FD::F>(bit) & f.empty;
+        const u64 t = (q1 | (sh<FD::F>(q1 & FD::ROW_AFTER1) & f.empty) | (pawn_attacks<STM>(bit) & f.them)) & line;
+        c += pc(t) + 3 * pc(t & FD::LAST);
+      } else if (bit & (f.O | f.D)) {
+        const Lines ls = lines_of(s);
+        const bool orth_line = (line == ls.file) || (line == ls.rank);
+        if ((orth_line && (bit & f.O)) || (!orth_line && (bit & f.D))) c += pc(line_attacks(s, line, f.occ) & notus);
+      }
+    }
+  }
+  const int ep = meta_ep(meta);
+  if (ep >= 0) {
+    u64 cand = pawn_attacks<1 - STM>(1ull << ep) & f.P;
+    while (cand) {
+      const int s = lsb(cand);
+      cand &= cand - 1;
+      c += ep_legal<STM>(f, a.ksq, s, ep, ep - FD::F) ? 1u : 0u;
+    }
+  }
+  ns_out = ns;
+  return c;
 }
 
 // Promotion piece -> kind code (1 N, 2 B, 3 R, 4 Q).

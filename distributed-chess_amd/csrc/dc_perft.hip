@@ -68,7 +68,8 @@ struct RefRules {
 #define DC_FIDE_MINB 2  // (A/B: 4 = the round-3 budget, 128 VGPRs with spills)
 #endif
 #ifndef DC_FIDE_SPLIT
-#define DC_FIDE_SPLIT 1  // k_count2b<FideRules>: simple children counted as c0 (fide_sens); 0: every child made
+#define DC_FIDE_SPLIT 1  // k_count2b<FideRules>: simple children counted as c0 (fide_sens); 0: every child
+                         // made; 2: the counting pass set-wise (fide_count_split) instead of enumerating
 #endif
 struct FideRules {
   static constexpr bool kMeta = true;
@@ -978,7 +979,12 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
         sens_masks(fide_sens<STM>(p, pm), m);
 #pragma unroll
         for (int k = 0; k < SN_COUNT; ++k) sh.sens[k][tid] = m[k];
+#if DC_FIDE_SPLIT == 2
+        u32 ns;
+        cnt = fide_count_split<STM>(p, pm, sens_at, ns);
+#else
         const u32 ns = fide_for_each_split<STM>(p, pm, sens_at, [&](int, int, int) { ++cnt; });
+#endif
         if (ns) simple_leaves = (u64)ns * fide_count<1 - STM>(p, pm & 15u);  // THEM to move, no en passant
       }
     } else {

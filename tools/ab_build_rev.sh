@@ -1,14 +1,18 @@
 #!/bin/bash
 # A/B baseline from a git revision: dc_perft.hip (and the headers it
-# includes) as of REV, linked with the working tree's other objects
-# (measurement only; tools/ab_perft_time.py times the libraries).
+# includes) as of REV (WT: the working tree), linked with the working tree's
+# other objects (measurement only; tools/ab_perft_time.py times the libraries).
 #   tools/ab_build_rev.sh NAME REV ["FLAGS"]
 # -> distributed-chess_amd/build/var/NAME/libdchess.so
 set -e
 N=$1; REV=$2; F=${3:-}
 R=$(cd "$(dirname "$0")/.." && pwd)
 T=$(mktemp -d)
-git -C $R archive $REV distributed-chess_amd/csrc include | tar -x -C $T
+if [ "$REV" = WT ]; then
+  (cd $R && tar -c distributed-chess_amd/csrc include) | tar -x -C $T
+else
+  git -C $R archive $REV distributed-chess_amd/csrc include | tar -x -C $T
+fi
 cd $R/distributed-chess_amd
 make -s libdchess.so
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -I$T/include"

@@ -15,7 +15,8 @@ or double push), S is not in check, and neither square is in the sets below
           also sees looking back, and that slider | the pin segments from O's
           king (first piece O's: up to and including the second piece)
   fsrc    (f only) first pieces seen from Z' toward d with an S slider of d's
-          kind behind them
+          kind behind them, and S pieces first on a line from O's king with
+          an O piece second (moving one may pin that piece)
   t_orth / t_diag   (t only, for rook/queen resp. bishop/queen movers) the
           open squares seen from Z' along orthogonal / diagonal lines
   lk, ln, lp        (king / knight / pawn movers) squares from which such an
@@ -151,6 +152,8 @@ def sens(pos):
         if blk and pos.cells[blk[0]] >> 3 == Ot:
             end = ray.index(blk[1]) + 1 if len(blk) > 1 else len(ray)
             allm |= sum(bit(q) for q in ray[:end] if q != blk[0])
+        elif len(blk) > 1 and pos.cells[blk[1]] >> 3 == Ot:
+            fsrc |= bit(blk[0])  # an S piece shielding an O piece: moving it may pin that piece
     allm |= fill(kind[Ot][R_] | kind[Ot][Q_], occ, ORTH) | fill(kind[Ot][B_] | kind[Ot][Q_], occ, DIAG)
     tp = kind[Ot][P_]
     fwd = 8 if Ot == 0 else -8
