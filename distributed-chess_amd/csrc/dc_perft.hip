@@ -68,8 +68,8 @@ struct RefRules {
 #define DC_FIDE_MINB 2  // (A/B: 4 = the round-3 budget, 128 VGPRs with spills)
 #endif
 #ifndef DC_FIDE_SPLIT
-#define DC_FIDE_SPLIT 1  // k_count2b<FideRules>: simple children counted as c0 (fide_sens); 0: every child
-                         // made; 2: the counting pass set-wise (fide_count_split) instead of enumerating
+#define DC_FIDE_SPLIT 2  // k_count2b<FideRules>: simple children counted as c0 (fide_sens); 0: every child
+                         // made; 1: the counting pass enumerates; 2: it counts set-wise (fide_count_split)
 #endif
 struct FideRules {
   static constexpr bool kMeta = true;
