@@ -112,8 +112,10 @@ def attacked_by(pos, col, target):
     return (att & target) != 0
 
 
-def sens(pos):
-    """The kernel's sets (fide_sens) as a dict, or None when no child is simple."""
+def sens(pos, split_og=False):
+    """The kernel's sets (fide_sens) as a dict, or None when no child is simple.
+    split_og: O's slider rays and pawn squares left out of "all" and returned
+    as "og" (the semi-simple class: only O's slider and pawn moves change)."""
     S, Ot = pos.stm, 1 - pos.stm
     side, kind = sets(pos.cells)
     occ = side[0] | side[1]
@@ -154,15 +156,17 @@ def sens(pos):
             allm |= sum(bit(q) for q in ray[:end] if q != blk[0])
         elif len(blk) > 1 and pos.cells[blk[1]] >> 3 == Ot:
             fsrc |= bit(blk[0])  # an S piece shielding an O piece: moving it may pin that piece
-    allm |= fill(kind[Ot][R_] | kind[Ot][Q_], occ, ORTH) | fill(kind[Ot][B_] | kind[Ot][Q_], occ, DIAG)
+    og = fill(kind[Ot][R_] | kind[Ot][Q_], occ, ORTH) | fill(kind[Ot][B_] | kind[Ot][Q_], occ, DIAG)
     tp = kind[Ot][P_]
     fwd = 8 if Ot == 0 else -8
     shf = (lambda b, n: (b << n) & FULL if n > 0 else b >> -n)
     after1 = 0xFF << 16 if Ot == 0 else 0xFF << 40
     push = shf(tp, fwd)
-    allm |= push | shf(push & after1, fwd) | pawn_att(tp, Ot)
+    og |= push | shf(push & after1, fwd) | pawn_att(tp, Ot)
+    if not split_og:
+        allm |= og
     return {"all": allm, "fsrc": fsrc, "t_orth": t_o, "t_diag": t_d, K_: leap_set(zp, DIRS),
-            N_: leap_set(zp, KNIGHT), P_: pawn_att(zp, Ot)}
+            N_: leap_set(zp, KNIGHT), P_: pawn_att(zp, Ot), "og": og}
 
 
 def simple_moves(pos, moves, sn):
