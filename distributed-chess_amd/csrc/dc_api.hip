@@ -1262,6 +1262,16 @@ static bool fused3_enabled() {
   return on;
 }
 
+// FIDE depth 5: the top kernel stops one ply short (DC_FIDE_TOP3=1, A/B only:
+// the round-4 plan, three plies in the one workgroup)
+static bool fide_top_short() {
+  static const bool on = [] {
+    const char* e = dc::ab_env("DC_FIDE_TOP3");
+    return !(e && e[0] == '1');
+  }();
+  return on;
+}
+
 // Enqueues one perft on the context stream up to (not including) the result
 // copy.  *host_sync is set when a level size had to be read back on the host
 // (exact mode or a level beyond the speculative budget): such a sequence
@@ -1291,6 +1301,11 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   const int final_plies = depth >= 3 ? 2 : 1;     // depth 1: no final stage
   const u32 S = std::max<u32>(1, std::min(split_depth, F));
   u32 T = exact ? 1 : std::min<u32>(F, 3);        // plies built by the single-workgroup top kernel
+  // FIDE depth 5 (F = 3): the final stage's parents (Kiwipete: 97,862) made
+  // inside the one workgroup were ~0.3 ms per position (rocprofv3, round 4);
+  // stopping the top kernel one ply short leaves them to k_make_count and
+  // k_level_write on every CU
+  if (fide && !exact && T == F && F == 3 && fide_top_short()) T = F - 1;
   if (sharded) T = std::min(T, S);
   static const u64 kTopCap[4] = {1, 256, 256 * 256, 1ull << 20};
   // buffers (allocated before anything is enqueued)
