@@ -1066,6 +1066,12 @@ __device__ __forceinline__ void sys_store(u32* p, u32 v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+#ifndef DC_LIVE_EXP
+#define DC_LIVE_EXP 0  // (measurement only) 1: validate answers V_OK without computing
+#endif
+#ifndef DC_LIVE_GATHER
+#define DC_LIVE_GATHER 0  // 1: n = 1 REF validate from cross-lane ballots (0: the board assembled in one lane)
+#endif
 // One request: lane e < n validates (applies) entry e; `fld(k, e)` reads
 // field k of entry e.  Writes the stamped response words.
 template <class F>
@@ -1094,7 +1100,13 @@ __device__ __forceinline__ void live_serve(LiveBox* box, u32 stamp, u32 n, bool 
     sys_store(&box->resp[18 * n + lane], sh | (u32)(uint8_t)p.ep);
   } else {
     const Board b{p.bb[0], p.bb[1], p.bb[2], p.bb[3]};
+#if DC_LIVE_EXP == 1
+    v = 0;  // (measurement only) no verdict work: the mailbox round trip alone
+    (void)b;
+    (void)mv;
+#else
     v = (uint8_t)(fide ? fide_verdict(b, p.stm & 1, pack_meta(p.castle, p.ep), mv) : ref_verdict(b, p.stm & 1, mv));
+#endif
   }
   sys_store(&box->resp[lane], (stamp << 16) | v | ((u32)info << 8));
 }
@@ -1118,7 +1130,30 @@ __global__ __launch_bounds__(64) void k_live(LiveBox* box, u32 seq, u64 lease_ti
         // the live consensus call: entry 0's fields are words 1..19, in the
         // lanes that polled them; lane 0 reads them across lanes (no LDS)
         if (__ballot(lane < words && (w0 >> 16) != stamp)) continue;  // still being written
-        live_serve(box, stamp, 1, apply, fide, lane, [&](u32 k) { return lane_bcast(w0, 1 + k) & 0xFFFFu; });
+        if (!apply && !fide && DC_LIVE_GATHER) {
+          // REF validate: the board's facts gathered across the lanes that
+          // polled its half-words (lane 1 + 4q + h: bits 16h.. of bb[q]), one
+          // ballot per fact, instead of assembling the board in one lane
+          // (that chain was ~0.5 us of a 3.3 us call, round 4)
+          const u32 mv = lane_bcast(w0, 19) & 0xFFFFu, stm = lane_bcast(w0, 17) & 1u;
+          const int f = (int)(mv & 63), t = (int)((mv >> 6) & 63), mid = (f + t) >> 1;
+          const u32 k = lane - 1u, c = w0 & 0xFFFFu, h = k & 3u;
+          const bool chunk = k < 16u;
+          const u64 bf = ballot(chunk && (u32)(f >> 4) == h && ((c >> (f & 15)) & 1u));
+          const u64 bt = ballot(chunk && (u32)(t >> 4) == h && ((c >> (t & 15)) & 1u));
+          const u64 bm = ballot(chunk && (u32)(mid >> 4) == h && ((c >> (mid & 15)) & 1u));
+          const u64 bb = ballot(chunk && k >= 4u && (c & ((u32)(between(f, t) >> (16 * h)) & 0xFFFFu)) != 0u);
+          auto nib_at = [](u64 B, int s) -> u32 {  // bit q of the nibble: lane 1 + 4q + (s >> 4)
+            const u64 x = B >> (1 + (s >> 4));
+            return (u32)(x & 1) | ((u32)(x >> 3) & 2u) | ((u32)(x >> 6) & 4u) | ((u32)(x >> 9) & 8u);
+          };
+          const u32 nib = nib_at(bf, f), nt = nib_at(bt, t), nm = nib_at(bm, mid);
+          const u32 t_occ = (nt >> 1) != 0u, mid_occ = (nm >> 1) != 0u;
+          const u32 v = ref_verdict_core(stm, mv, nib, t_occ, t_occ & (u32)((nt & 1u) == stm), mid_occ, (u32)(bb == 0));
+          if (lane == 0) sys_store(&box->resp[0], (stamp << 16) | v);
+        } else {
+          live_serve(box, stamp, 1, apply, fide, lane, [&](u32 k) { return lane_bcast(w0, 1 + k) & 0xFFFFu; });
+        }
       } else {
         bool torn = false;
         for (u32 base = 0; base < words; base += 64) {

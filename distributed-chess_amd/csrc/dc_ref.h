@@ -714,18 +714,16 @@ __device__ __forceinline__ void ref_make(Board& b, int f, int t) {
 // validate_move on one (position, move word).  Verdict order chess.rs:82-125.
 // Branch-free: every per-kind rule (chess.rs:214-360) is evaluated as a
 // predicate and the mover's kind selects one, so lanes holding different
-// pieces never serialise on a switch.
-__device__ __forceinline__ u32 ref_verdict(const Board& b, u32 stm, u32 m) {
+// pieces never serialise on a switch.  The core takes the board's facts the
+// rules read -- the mover's nibble, t occupied / own, the double push's mid
+// square occupied, the squares between f and t empty -- so the live validator
+// can gather them across lanes instead of assembling the board.
+__device__ __forceinline__ u32 ref_verdict_core(u32 stm, u32 m, u32 nib, u32 t_occ, u32 t_own, u32 mid_occ, u32 clear) {
   const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
-  const u32 nib = nibble(b, f);
   const u32 kind = nib >> 1;
-  const u64 occ = occupied(b);
-  const u64 own = stm ? b.b0 : (occ & ~b.b0);
-  const u32 t_occ = (u32)(occ >> t) & 1, t_own = (u32)(own >> t) & 1;
   const int dx = (t >> 3) - (f >> 3), dy = (t & 7) - (f & 7);
   const int ax = dx < 0 ? -dx : dx, ay = dy < 0 ? -dy : dy;
   const int dir = stm ? -1 : 1;
-  const u32 mid_occ = (u32)(occ >> ((f + t) >> 1)) & 1;  // only meaningful for a double push
   const u32 on_start = (u32)((f >> 3) == (stm ? 6 : 1));
   const u32 push = (u32)(dy == 0) & (u32)(dx == dir) & (t_occ ^ 1);
   const u32 dbl = (u32)(dy == 0) & (u32)(dx == 2 * dir) & on_start & (t_occ ^ 1) & (mid_occ ^ 1);
@@ -735,7 +733,6 @@ __device__ __forceinline__ u32 ref_verdict(const Board& b, u32 stm, u32 m) {
   const u32 king_ok = (u32)(ax <= 1) & (u32)(ay <= 1);
   const u32 orth = (u32)(dx == 0) | (u32)(dy == 0);
   const u32 diag = (u32)(ax == ay);
-  const u32 clear = (u32)((between(f, t) & occ) == 0);
   // kind codes: P=1 N=2 K=3 X=4 B=5 R=6 Q=7
   const u32 line_ok = ((kind == KC_B) ? diag : (kind == KC_R) ? orth : (kind == KC_Q) ? (orth | diag) : 0u) & clear;
   const u32 step_ok = (kind == KC_P) ? pawn_ok : (kind == KC_N) ? knight_ok : (kind == KC_K) ? king_ok : 0u;
@@ -745,6 +742,16 @@ __device__ __forceinline__ u32 ref_verdict(const Board& b, u32 stm, u32 m) {
   v = (kind == 0) ? V_NO_PIECE : v;
   v = (m & 0x8000u) ? V_OOR : v;
   return v;
+}
+
+__device__ __forceinline__ u32 ref_verdict(const Board& b, u32 stm, u32 m) {
+  const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
+  const u64 occ = occupied(b);
+  const u64 own = stm ? b.b0 : (occ & ~b.b0);
+  const u32 t_occ = (u32)(occ >> t) & 1, t_own = (u32)(own >> t) & 1;
+  const u32 mid_occ = (u32)(occ >> ((f + t) >> 1)) & 1;  // only meaningful for a double push
+  const u32 clear = (u32)((between(f, t) & occ) == 0);
+  return ref_verdict_core(stm, m, nibble(b, f), t_occ, t_own, mid_occ, clear);
 }
 
 __device__ __forceinline__ u64 board_digest(const Board& b, u32 stm) {
