@@ -1070,7 +1070,7 @@ __device__ __forceinline__ void sys_store(u32* p, u32 v) {
 #define DC_LIVE_EXP 0  // (measurement only) 1: validate answers V_OK without computing
 #endif
 #ifndef DC_LIVE_GATHER
-#define DC_LIVE_GATHER 0  // 1: n = 1 REF validate from cross-lane ballots (0: the board assembled in one lane)
+#define DC_LIVE_GATHER 1  // n = 1 REF validate from cross-lane ballots (0: the board assembled in one lane)
 #endif
 // One request: lane e < n validates (applies) entry e; `fld(k, e)` reads
 // field k of entry e.  Writes the stamped response words.
@@ -1134,7 +1134,7 @@ __global__ __launch_bounds__(64) void k_live(LiveBox* box, u32 seq, u64 lease_ti
           // REF validate: the board's facts gathered across the lanes that
           // polled its half-words (lane 1 + 4q + h: bits 16h.. of bb[q]), one
           // ballot per fact, instead of assembling the board in one lane
-          // (that chain was ~0.5 us of a 3.3 us call, round 4)
+          // (3.16-3.19 -> 3.06-3.12 us median per call, same box, round 4)
           const u32 mv = lane_bcast(w0, 19) & 0xFFFFu, stm = lane_bcast(w0, 17) & 1u;
           const int f = (int)(mv & 63), t = (int)((mv >> 6) & 63), mid = (f + t) >> 1;
           const u32 k = lane - 1u, c = w0 & 0xFFFFu, h = k & 3u;
