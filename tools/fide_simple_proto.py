@@ -39,6 +39,7 @@ sys.path.insert(0, os.path.join(HERE, "..", "tests"))
 import oracle_lib as O  # noqa: E402
 
 FULL = (1 << 64) - 1
+PIN_PRECISE = os.environ.get("FIDE_PIN_PRECISE") == "1"  # (study) pin segments only where a pin exists
 P_, N_, B_, R_, Q_, K_ = range(6)
 ORTH = ((1, 0), (-1, 0), (0, 1), (0, -1))
 DIAG = ((1, 1), (1, -1), (-1, 1), (-1, -1))
@@ -153,7 +154,19 @@ def sens(pos, split_og=False):
         blk = [q for q in ray if occ >> q & 1]
         if blk and pos.cells[blk[0]] >> 3 == Ot:
             end = ray.index(blk[1]) + 1 if len(blk) > 1 else len(ray)
-            allm |= sum(bit(q) for q in ray[:end] if q != blk[0])
+            seg = sum(bit(q) for q in ray[:end] if q != blk[0])
+            if not PIN_PRECISE or (len(blk) > 1 and st >> blk[1] & 1):
+                allm |= seg  # a pin: any change on it can break it
+            else:
+                # no pin yet: a slider of the line's kind landing past the O piece
+                # (before the next piece) makes one, and so can the next piece leaving
+                past = sum(bit(q) for q in ray[ray.index(blk[0]) + 1:end] if len(blk) < 2 or q != blk[1])
+                if di < 4:
+                    t_o |= past
+                else:
+                    t_d |= past
+                if len(blk) > 1:
+                    fsrc |= bit(blk[1])
         elif len(blk) > 1 and pos.cells[blk[1]] >> 3 == Ot:
             fsrc |= bit(blk[0])  # an S piece shielding an O piece: moving it may pin that piece
     og = fill(kind[Ot][R_] | kind[Ot][Q_], occ, ORTH) | fill(kind[Ot][B_] | kind[Ot][Q_], occ, DIAG)
