@@ -186,13 +186,21 @@ __device__ __forceinline__ void scan_dir(const FPos<STM>& f, int ksq, const Line
 #ifndef DC_FIDE_SNIPER
 #define DC_FIDE_SNIPER 1
 #endif
+#ifndef DC_FIDE_LAZY_DANGER
+#define DC_FIDE_LAZY_DANGER 0  // 1: fide_count computes the attack map only in waves that need it (2: also the split's passes)
+#endif
+// with_danger = false (wave-uniform): no attack map; danger reads "every
+// square attacked", i.e. no king move and no castling -- for callers whose
+// lanes have neither a free square next to the king nor an open castling path
 template <int STM, bool TAB = false>
-__device__ __forceinline__ Analysis analyse(const FPos<STM>& f) {
+__device__ __forceinline__ Analysis analyse(const FPos<STM>& f, bool with_danger = true) {
   constexpr int THEM = 1 - STM;
   Analysis a;
   const u64 empty_nk = f.empty | f.K;
-  a.danger = pawn_attacks<THEM>(f.tP) | knight_attacks_t<TAB>(f.tN) | king_attacks_t<TAB>(f.tK) |
-             orth_attacks(f.tO, empty_nk) | diag_attacks(f.tD, empty_nk);
+  a.danger = ~0ull;
+  if (with_danger)
+    a.danger = pawn_attacks<THEM>(f.tP) | knight_attacks_t<TAB>(f.tN) | king_attacks_t<TAB>(f.tK) |
+               orth_attacks(f.tO, empty_nk) | diag_attacks(f.tD, empty_nk);
   a.checkers = 0;
   a.pinned = 0;
   a.ksq = f.K ? lsb(f.K) : -1;
@@ -286,6 +294,18 @@ struct FDir {
   static constexpr u32 RQ = STM ? CR_BQ : CR_WQ;
 };
 
+// Does any lane of the wave need the attack map: a free square next to the
+// king or an open castling path (`meta`'s rights, the squares between king
+// and rook empty)?
+template <int STM>
+__device__ __forceinline__ bool wave_needs_danger(const FPos<STM>& f, u32 meta) {
+  typedef FDir<STM> FD;
+  const int h = FD::HOME;
+  const bool castle_open = ((f.K >> h) & 1) && (((meta & FD::RK) && !((f.occ >> (h + 1)) & 3)) ||
+                                                 ((meta & FD::RQ) && !((f.occ >> (h - 3)) & 7)));
+  return __ballot((king_attacks(f.K) & ~f.us) != 0 || castle_open) != 0;
+}
+
 // Castling targets (king destination squares) -- only when not in check.
 template <int STM>
 __device__ __forceinline__ u64 castle_targets(const FPos<STM>& f, const Analysis& a, u32 meta, const Board& b) {
@@ -307,7 +327,15 @@ template <int STM, bool TAB = false>
 __device__ __forceinline__ u32 fide_count(const Board& b, u32 meta) {
   typedef FDir<STM> FD;
   const FPos<STM> f = fpos<STM>(b);
+  // the attack map is needed only for king moves and castling: a wave none of
+  // whose lanes has a free square next to its king or an open castling path
+  // skips it (a third of perft(7)'s leaf parents; siblings share their king's
+  // surroundings)
+#if DC_FIDE_LAZY_DANGER
+  const Analysis a = analyse<STM, TAB>(f, wave_needs_danger<STM>(f, meta));
+#else
   const Analysis a = analyse<STM, TAB>(f);
+#endif
   const u64 notus = ~f.us;
   u32 c = pc(king_attacks_t<TAB>(f.K) & notus & ~a.danger);
   if (a.checkers & (a.checkers - 1)) return c;  // double check: king moves only
@@ -591,7 +619,7 @@ template <int STM, class SensAt, class Visit>
 __device__ __forceinline__ u32 fide_for_each_split(const Board& b, u32 meta, SensAt&& sn, Visit&& visit) {
   typedef FDir<STM> FD;
   const FPos<STM> f = fpos<STM>(b);
-  const Analysis a = analyse<STM>(f);
+  const Analysis a = analyse<STM>(f, DC_FIDE_LAZY_DANGER < 2 || wave_needs_danger<STM>(f, meta));
   const u64 notus = ~f.us;
   u32 ns = 0;
   auto emit = [&](int from, u64 targets) {
@@ -723,7 +751,7 @@ template <int STM, class SensAt>
 __device__ __forceinline__ u32 fide_count_split(const Board& b, u32 meta, SensAt&& sn, u32& ns_out) {
   typedef FDir<STM> FD;
   const FPos<STM> f = fpos<STM>(b);
-  const Analysis a = analyse<STM>(f);
+  const Analysis a = analyse<STM>(f, DC_FIDE_LAZY_DANGER < 2 || wave_needs_danger<STM>(f, meta));
   const u64 notus = ~f.us;
   u32 c = 0, ns = 0;
   if (a.ksq >= 0) {
