@@ -187,7 +187,8 @@ __device__ __forceinline__ void scan_dir(const FPos<STM>& f, int ksq, const Line
 #define DC_FIDE_SNIPER 1
 #endif
 #ifndef DC_FIDE_LAZY_DANGER
-#define DC_FIDE_LAZY_DANGER 0  // 1: fide_count computes the attack map only in waves that need it (2: also the split's passes)
+#define DC_FIDE_LAZY_DANGER 0  // 1: fide_count computes the attack map only in waves that need it (2: also
+                               // the split's passes) -- measured slower, off
 #endif
 // with_danger = false (wave-uniform): no attack map; danger reads "every
 // square attacked", i.e. no king move and no castling -- for callers whose
