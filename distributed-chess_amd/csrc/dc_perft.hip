@@ -943,6 +943,29 @@ struct C2bShared {
   u64 sens[SPLIT ? SN_COUNT : 1][256];  // sens_masks, [set][parent]
 };
 
+// DC_DIAG_CHILD (diagnostic builds only, never the product):
+// every child k_count2b counts is written as one 64-byte record at a position
+// fixed by (block, chunk, slot) -- no atomics, so the kernel's timing changes
+// only by the stores -- for tools/fide_child_diag.py to recount on the host.
+// DC_DIAG_CHILD == 2 also counts each child a second time (same code, an
+// opaque copy of the board in between) and records both counts; == 3 writes
+// the count alone (one dword per child at the same position).
+#ifdef DC_DIAG_CHILD
+struct DiagRec {
+  u64 b[4];
+  u32 cm, k, k2, e;  // e: the slot word | STM << 31
+  u32 pidx, hwid, xcc, misc;  // misc: active lanes | lane << 8 | wave << 16 | (window > 0) << 24
+};
+static_assert(sizeof(DiagRec) == 64, "diag record");
+__device__ DiagRec* g_diag_rec;
+__device__ u64 g_diag_cap;
+extern "C" __attribute__((visibility("default"))) int dc_diag_child_set(void* dev_recs, u64 cap) {
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_rec), &dev_recs, sizeof(dev_recs)) != hipSuccess) return -1;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(g_diag_cap), &cap, sizeof(cap)) != hipSuccess) return -1;
+  return 0;
+}
+#endif
+
 template <class R, int STM>
 __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
@@ -958,6 +981,9 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
   const u64 lo = rng->lo, hi = rng->hi;
   const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;
   const u64 blo = min(hi, lo + (u64)blockIdx.x * per), bhi = min(hi, blo + per);
+#ifdef DC_DIAG_CHILD
+  u64 diag_off = (u64)blockIdx.x * per * 218;  // 218: the most legal moves of any position
+#endif
   for (u64 s = blo; s < bhi; s += kChunk) {
     const u64 i = s + tid;
     const bool valid = i < bhi;
@@ -1036,9 +1062,52 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
           const u32 ptag = sh.ptag[pl];
           if (ptag == tag0) acc += k;
           else if (k) atomicAdd((unsigned long long*)&sh.hist[ptag], (unsigned long long)k);
+#ifdef DC_DIAG_CHILD
+          {
+            DiagRec* rec = g_diag_rec;
+            const u64 at = diag_off + base + r;
+#if DC_DIAG_CHILD == 3
+            // the count alone, one dword at the record's position (the least
+            // perturbing form; the children are identified by a full-record run)
+            if (rec && at < g_diag_cap) reinterpret_cast<u32*>(rec)[at] = k;
+            if (false) {
+#else
+            if (rec && at < g_diag_cap) {
+#endif
+              u32 k2 = k;
+#if DC_DIAG_CHILD == 2
+              Board c2 = ch;
+              u32 cm2 = cm;
+              asm volatile("" : "+v"(c2.b0), "+v"(c2.b1), "+v"(c2.b2), "+v"(c2.b3), "+v"(cm2));
+              k2 = R::template count_final<1 - STM>(c2, cm2);
+#endif
+              u32 hwid, xcc;
+              asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+              asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+              const u64 ex = __builtin_amdgcn_read_exec();
+              DiagRec d;
+              d.b[0] = ch.b0;
+              d.b[1] = ch.b1;
+              d.b[2] = ch.b2;
+              d.b[3] = ch.b3;
+              d.cm = cm;
+              d.k = k;
+              d.k2 = k2;
+              d.e = (e & 0x7FFFFFFFu) | ((u32)STM << 31);
+              d.pidx = (u32)(s + pl);
+              d.hwid = hwid;
+              d.xcc = xcc;
+              d.misc = (u32)__popcll(ex) | ((tid & 63) << 8) | ((tid >> 6) << 16) | ((base ? 1u : 0u) << 24);
+              rec[at] = d;
+            }
+          }
+#endif
         }
       }
     }
+#ifdef DC_DIAG_CHILD
+    diag_off += total;
+#endif
     tag_hist_add(sh.hist, tag0, acc, true);
     __syncthreads();  // par/ptag/slot reused by the next chunk
   }

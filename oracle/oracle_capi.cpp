@@ -236,4 +236,27 @@ uint64_t or_fast_digest(const int8_t* cells, uint8_t stm) {
   return fastcpu::digest(p);
 }
 
+// Legal-move counts of n quad-bitboard positions (bb[4*i..4*i+3], the device
+// Board layout; meta: castle rights | ep square << 4 | 0x400 when valid) --
+// the per-child recount of tools/fide_child_diag.py.
+void or_fast_count_quad(const uint64_t* bb, const uint8_t* stm, const uint16_t* meta, uint32_t n, int rules,
+                        unsigned threads, uint32_t* out) {
+  static const int8_t kind_of_code[8] = {-1, fastcpu::P, fastcpu::N, fastcpu::K, fastcpu::X,
+                                         fastcpu::B, fastcpu::R, fastcpu::Q};
+  par(n, threads, [&](size_t i) {
+    const uint64_t* q = bb + 4 * i;
+    fastcpu::Pos p;
+    for (int s = 0; s < 64; ++s) {
+      const int code = static_cast<int>(((q[1] >> s) & 1) | (((q[2] >> s) & 1) << 1) | (((q[3] >> s) & 1) << 2));
+      p.sq[s] = code ? static_cast<int8_t>(((q[0] >> s) & 1) * 8 + kind_of_code[code]) : int8_t(-1);
+    }
+    p.stm = stm[i];
+    const uint16_t m = meta ? meta[i] : 0;
+    p.castle = static_cast<uint8_t>(m & 15);
+    p.ep = (m & 0x400) ? static_cast<int8_t>((m >> 4) & 63) : int8_t(-1);
+    fastcpu::Move ms[256];
+    out[i] = static_cast<uint32_t>(fastcpu::gen_moves(p, static_cast<fastcpu::Rules>(rules), ms));
+  });
+}
+
 }  // extern "C"

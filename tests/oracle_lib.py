@@ -59,6 +59,7 @@ def lib():
         L.or_fast_quad.argtypes = [_i8p, _u64p]
         L.or_fast_digest.restype = C.c_uint64
         L.or_fast_digest.argtypes = [_i8p, C.c_uint8]
+        L.or_fast_count_quad.argtypes = [_u64p, _u8p, _u16p, C.c_uint32, C.c_int, C.c_uint, _u32p]
         _LIB = L
     return _LIB
 
@@ -204,3 +205,15 @@ def quad(cells):
 def digest(cells, stm):
     cells = np.ascontiguousarray(cells, dtype=np.int8)
     return int(lib().or_fast_digest(_p(cells, _i8p), stm))
+
+
+def fast_count_quad(bb, stm, meta, rules=FIDE, threads=None):
+    """Legal-move counts of quad-bitboard positions: bb (n, 4) u64, stm (n,) u8, meta (n,) u16."""
+    bb = np.ascontiguousarray(bb, dtype=np.uint64)
+    stm = np.ascontiguousarray(stm, dtype=np.uint8)
+    meta = np.ascontiguousarray(meta, dtype=np.uint16)
+    n = len(stm)
+    out = np.zeros(n, dtype=np.uint32)
+    lib().or_fast_count_quad(_p(bb, _u64p), _p(stm, _u8p), _p(meta, _u16p), n, rules,
+                             threads or os.cpu_count() or 1, _p(out, _u32p))
+    return out

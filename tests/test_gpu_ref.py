@@ -18,6 +18,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 KA = json.load(open(os.path.join(GOLD, "known_answers.json")))
 OG = json.load(open(os.path.join(GOLD, "oracle_golden.json")))
 REF_DEEP = json.load(open(os.path.join(GOLD, "ref_deep.json")))
+REF_D6 = json.load(open(os.path.join(GOLD, "ref_d6.json")))["positions"]
 
 
 def sha(a):
@@ -493,6 +494,30 @@ def test_perft_suite_fens_ref_rules(engine):
         p = dchess.pos_from_fen(e["fen"])
         for d in ("3", "5"):
             assert engine.perft(p, int(d))[0] == e["perft"][d], (name, d)
+
+
+@pytest.mark.parametrize("name", sorted(REF_D6))
+def test_perft6_ref_off_startpos_tree(engine, name):
+    """REF perft(6) with divide of the six suite FENs and ten mid-game boards
+    (four edited: no white king, no kings, unknown-kind pieces, two white
+    kings -- chess.rs:199-212, 350-360), fastcpu-pinned and refcpu-checked on a
+    subtree each (tests/golden/make_ref_d6_golden.py).  Their final stage runs
+    k_count3c on a full grid (0.3M-9M move words) where the startpos goldens
+    were the only full-occupancy pins; then again as 8 strided shards cut after
+    the top kernel, whose divides must sum to the same vector."""
+    e = REF_D6[name]
+    p = dchess.pos_from_cells(np.array(e["cells"], np.int8), e["stm"])
+    tot, div, rm = engine.perft(p, 6)
+    assert tot == e["total"]
+    assert {str(int(m)): int(v) for m, v in zip(rm, div)} == e["divide"]
+    acc, t = {}, 0
+    for k in range(8):
+        st, sd, srm = engine.perft_shard(p, 6, 3, k, 8)
+        t += st
+        for m, v in zip(srm, sd):
+            acc[str(int(m))] = acc.get(str(int(m)), 0) + int(v)
+    assert t == e["total"]
+    assert {m: v for m, v in acc.items() if v} == {m: v for m, v in e["divide"].items() if v}
 
 
 # ------------------------------------------------------------- replicas (C1)

@@ -160,3 +160,21 @@ def test_replay_properties():
 
 def test_startpos_quad_golden():
     assert [int(x) for x in O.quad(O.startpos_cells())] == OG["startpos_quad"]
+
+
+REF_D6 = json.load(open(os.path.join(GOLD, "ref_d6.json")))["positions"]
+
+
+@pytest.mark.parametrize("name", sorted(REF_D6))
+def test_ref_d6_golden_consistent(name):
+    """tests/golden/ref_d6.json (REF perft(6) off the startpos tree): the divide
+    sums to the total, the root moves are fastcpu's, and refcpu (the literal
+    chess.rs restatement) agrees with fastcpu at depth 2 of the same board."""
+    e = REF_D6[name]
+    p = O.Pos(np.array(e["cells"], np.int8), e["stm"], 0, -1)
+    assert sum(e["divide"].values()) == e["total"]
+    _, _, rm = O.fast_perft(p, 1, O.REF, threads=2)
+    assert sorted(str(int(m)) for m in rm) == sorted(e["divide"])
+    ft, _, _ = O.fast_perft(p, 2, O.REF, threads=2)
+    rt, _ = O.ref_perft(p.cells, p.stm, 2, threads=2)
+    assert ft == rt

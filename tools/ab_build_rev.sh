@@ -2,7 +2,7 @@
 # A/B baseline from a git revision: dc_perft.hip (and the headers it
 # includes) as of REV (WT: the working tree), linked with the working tree's
 # other objects (measurement only; tools/ab_perft_time.py times the libraries).
-#   [SRCS="dc_perft dc_api"] tools/ab_build_rev.sh NAME REV ["FLAGS"]
+#   [SRCS="dc_perft dc_api"] [PATCH="cmd"] tools/ab_build_rev.sh NAME REV ["FLAGS"]
 # (SRCS: the sources taken from REV, default dc_perft)
 # -> distributed-chess_amd/build/var/NAME/libdchess.so
 set -e
@@ -14,6 +14,8 @@ if [ "$REV" = WT ]; then
 else
   git -C $R archive $REV distributed-chess_amd/csrc include | tar -x -C $T
 fi
+# PATCH: a command run in the exported tree before building (diagnostics)
+if [ -n "${PATCH:-}" ]; then (cd $T && eval "$PATCH"); fi
 cd $R/distributed-chess_amd
 make -s libdchess.so
 HIPFLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wno-unused-function -I$T/include"
