@@ -16,6 +16,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -40,12 +41,23 @@ static_assert(sizeof(dc_pos) == sizeof(DevPos), "dc_pos / DevPos layout");
 // pointers and are re-captured after a bump.
 static std::atomic<uint64_t> g_alloc_epoch{0};
 
+// hipFree (and hipHostFree) wait for every stream of the device, a resident
+// live-validator wave's included (dc_live_validator): a buffer grown or freed
+// while any context's wave runs would block for that wave's lease (up to 60 s).
+// LiveHold stops every resident wave of the process first and keeps new ones
+// from starting while it is held (those calls take the launched path).
+struct LiveHold {
+  LiveHold();
+  ~LiveHold();
+};
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
   size_t cap = 0;
   hipError_t ensure(size_t n) {
     if (n <= cap) return hipSuccess;
+    LiveHold hold;
     g_alloc_epoch.fetch_add(1);
     if (p) (void)hipFree(p);
     p = nullptr;
@@ -61,7 +73,10 @@ struct DBuf {
     return hipSuccess;
   }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      LiveHold hold;
+      (void)hipFree(p);
+    }
     p = nullptr;
     cap = 0;
   }
@@ -129,6 +144,8 @@ struct dc_ctx {
   uint32_t live_seq = 0;
   uint32_t live_lease_us = 0;
   bool live_running = false;
+  uint32_t live_timeout_us = 5000000;  // a call the wave neither answers nor leaves in this long is DC_EHIP
+  std::mutex live_mu;  // the wave's state: held by live calls and by LiveHold's stop from another thread
   // The last perft launch sequence, captured as a hipGraph (see perft_run).
   struct PerftKey {
     u32 rules, depth, split, shard, n_shards, stm, k4;
@@ -189,6 +206,7 @@ struct dc_ctx {
   bool gtab_ready = false;
 
   ~dc_ctx() {
+    LiveHold hold;  // pinned host frees below wait for every stream too
     tx_text.release();
     tx_off.release();
     tx_act.release();
@@ -335,6 +353,16 @@ static int enter(dc_ctx* c) {
     if (_r != DC_SUCCESS) return _r;  \
   } while (0)
 
+// Device work other than a live call: every resident live-validator wave of
+// the process is stopped first and stays stopped for the call (LiveHold).
+// HIP maps a process's streams onto at most GPU_MAX_HW_QUEUES (4) hardware
+// queues, so a kernel launched on a stream that shares its queue with a
+// resident wave would wait behind that wave for its whole lease (round 5:
+// a perft blocked 20 s behind two 20 s leases in the live test module).
+#define ENTER_WORK(c) \
+  ENTER(c);           \
+  LiveHold live_hold_
+
 // ================================================================ context
 extern "C" {
 
@@ -385,11 +413,22 @@ int dc_ctx_create(int device, dc_ctx** out) {
 }
 
 static int live_stop(dc_ctx* c);
+// Contexts with the live validator on (registered by dc_live_validator,
+// removed by dc_ctx_destroy) and the number of LiveHolds alive.  Lock order:
+// g_live_mu, then a context's live_mu.
+static std::mutex g_live_mu;
+static std::set<dc_ctx*> g_live_ctxs;
+static std::atomic<int> g_live_hold{0};
 
 int dc_ctx_destroy(dc_ctx* c) {
   if (!c) return DC_EINVAL;
   (void)hipSetDevice(c->device);
-  (void)live_stop(c);
+  {
+    std::lock_guard<std::mutex> g(g_live_mu);
+    std::lock_guard<std::mutex> l(c->live_mu);
+    (void)live_stop(c);
+    g_live_ctxs.erase(c);
+  }
   (void)hipStreamSynchronize(c->stream);
   delete c;
   return DC_SUCCESS;
@@ -424,7 +463,7 @@ int dc_ctx_reset_stats(dc_ctx* c) {
 }
 
 int dc_device_alloc(dc_ctx* c, size_t bytes, void** d_ptr) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (!d_ptr) return DC_EINVAL;
   *d_ptr = nullptr;
   HIP_TRY(hipMalloc(d_ptr, std::max<size_t>(bytes, 1)));
@@ -432,20 +471,20 @@ int dc_device_alloc(dc_ctx* c, size_t bytes, void** d_ptr) {
 }
 
 int dc_device_free(dc_ctx* c, void* d_ptr) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (d_ptr) HIP_TRY(hipFree(d_ptr));
   return DC_SUCCESS;
 }
 
 int dc_memcpy_h2d(dc_ctx* c, void* d_dst, const void* src, size_t bytes) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (bytes && (!d_dst || !src)) return DC_EINVAL;
   if (bytes) HIP_TRY(hipMemcpyAsync(d_dst, src, bytes, hipMemcpyHostToDevice, c->stream));
   return sync_ctx(c);
 }
 
 int dc_memcpy_d2h(dc_ctx* c, void* dst, const void* d_src, size_t bytes) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (bytes && (!dst || !d_src)) return DC_EINVAL;
   if (bytes) HIP_TRY(hipMemcpyAsync(dst, d_src, bytes, hipMemcpyDeviceToHost, c->stream));
   return sync_ctx(c);
@@ -587,6 +626,16 @@ static int live_stop(dc_ctx* c) {
   return e == hipSuccess ? DC_SUCCESS : DC_EHIP;
 }
 
+LiveHold::LiveHold() {
+  g_live_hold.fetch_add(1);
+  std::lock_guard<std::mutex> g(g_live_mu);
+  for (dc_ctx* c : g_live_ctxs) {
+    std::lock_guard<std::mutex> l(c->live_mu);
+    (void)live_stop(c);
+  }
+}
+LiveHold::~LiveHold() { g_live_hold.fetch_sub(1); }
+
 static int live_start(dc_ctx* c) {
   __atomic_store_n(&c->live->state, 0u, __ATOMIC_RELEASE);
   __atomic_store_n(&c->live->ctl, 0u, __ATOMIC_RELEASE);
@@ -597,28 +646,54 @@ static int live_start(dc_ctx* c) {
 
 int dc_live_validator(dc_ctx* c, uint32_t lease_us) {
   ENTER(c);
-  if (lease_us == 0) {
-    const int e = live_stop(c);
-    c->live_lease_us = 0;
-    return e;
-  }
   if (lease_us > 60u * 1000 * 1000) return DC_EINVAL;  // at most a minute
-  if (!c->live) {
+  if (lease_us && !c->live) {
     HIP_TRY(hipHostMalloc((void**)&c->live, sizeof(dc::LiveBox), hipHostMallocCoherent));
     std::memset((void*)c->live, 0, sizeof(dc::LiveBox));
   }
-  if (!c->live_stream) HIP_TRY(hipStreamCreateWithFlags(&c->live_stream, hipStreamNonBlocking));
+  if (lease_us && !c->live_stream) HIP_TRY(hipStreamCreateWithFlags(&c->live_stream, hipStreamNonBlocking));
+  std::lock_guard<std::mutex> g(g_live_mu);
+  std::lock_guard<std::mutex> l(c->live_mu);
+  if (lease_us == 0) {
+    const int e = live_stop(c);
+    c->live_lease_us = 0;
+    g_live_ctxs.erase(c);
+    return e;
+  }
   if (c->live_running && lease_us != c->live_lease_us) {
     const int e = live_stop(c);  // the running wave holds the old lease
     if (e != DC_SUCCESS) return e;
   }
   c->live_lease_us = lease_us;
+  g_live_ctxs.insert(c);
+  return DC_SUCCESS;
+}
+
+// Test hook (not in the header): the live call's no-answer timeout, so a test
+// can force the timeout path and check the next call's verdicts.
+extern "C" __attribute__((visibility("default"))) int dc_test_live_timeout(dc_ctx* c, uint32_t us) {
+  if (!c) return DC_EINVAL;
+  std::lock_guard<std::mutex> l(c->live_mu);
+  c->live_timeout_us = us;
   return DC_SUCCESS;
 }
 
 // One request through the mailbox.  pos_out (apply) may alias pos.
 static int live_call(dc_ctx* c, bool apply, bool fide, const dc_pos* pos, const uint16_t* moves, uint32_t n,
                      uint8_t* verdicts, uint8_t* info, dc_pos* pos_out) {
+  // About to start a wave: the process keeps one resident at a time, since
+  // two contexts' live streams may share a hardware queue, where the second
+  // wave would wait behind the first for its whole lease.
+  std::unique_lock<std::mutex> g(g_live_mu, std::defer_lock);
+  if (!c->live_running) {
+    g.lock();
+    for (dc_ctx* o : g_live_ctxs)
+      if (o != c) {
+        std::lock_guard<std::mutex> l(o->live_mu);
+        (void)live_stop(o);
+      }
+  }
+  std::lock_guard<std::mutex> lock(c->live_mu);
   dc::LiveBox* b = c->live;
   if (!c->live_running) {
     const int e = live_start(c);
@@ -655,8 +730,13 @@ static int live_call(dc_ctx* c, bool apply, bool fide, const dc_pos* pos, const 
         if (complete()) break;
         const int e = live_start(c);
         if (e != DC_SUCCESS) return e;
-      } else if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+      } else if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(c->live_timeout_us)) {
         (void)live_stop(c);
+        // the request may still be in the mailbox, and a wave on its way out
+        // may have answered it: clear it and burn its stamp, so the next
+        // call's wave looks for seq + 1 and never takes this one for its own
+        __atomic_store_n(&b->req[0], 0u, __ATOMIC_RELEASE);
+        c->live_seq = seq;
         return DC_EHIP;  // the wave neither answered nor stopped
       }
     }
@@ -681,7 +761,7 @@ static int live_call(dc_ctx* c, bool apply, bool fide, const dc_pos* pos, const 
 }
 
 static bool live_eligible(const dc_ctx* c, uint32_t n) {
-  return c->live_lease_us && n <= dc::kLiveMax && !c->profiling;
+  return c->live_lease_us && n <= dc::kLiveMax && !c->profiling && g_live_hold.load() == 0;
 }
 
 // ============================================================== validation
@@ -691,6 +771,7 @@ int dc_validate_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, const uint16
   if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
   if (n == 0) return DC_SUCCESS;
   if (live_eligible(c, n)) return live_call(c, false, rules == DC_RULES_FIDE, pos, moves, n, verdicts, nullptr, nullptr);
+  LiveHold live_hold_;  // the launched path (ENTER_WORK)
   if (n <= kHostIoBatch) {  // pinned, read in place by the kernel
     if (!c->host_io) {
       HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo), hipHostMallocCoherent));
@@ -731,6 +812,7 @@ int dc_apply_batch(dc_ctx* c, uint32_t rules, dc_pos* pos, const uint16_t* moves
   if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
   if (n == 0) return DC_SUCCESS;
   if (live_eligible(c, n)) return live_call(c, true, rules == DC_RULES_FIDE, pos, moves, n, verdicts, info, pos);
+  LiveHold live_hold_;  // the launched path (ENTER_WORK)
   if (n <= kHostIoBatch) {  // pinned, read and written in place by the kernel
     if (!c->host_io) {
       HIP_TRY(hipHostMalloc((void**)&c->host_io, sizeof(HostIo), hipHostMallocCoherent));
@@ -819,7 +901,7 @@ static int replay_impl(dc_ctx* c, uint32_t rules, const dc_pos* start, const uin
 
 int dc_replay_device(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* d_moves, uint32_t n_games,
                      uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests, dc_replay_stats* stats) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (rules > DC_RULES_FIDE || (n_games && n_plies && !d_moves)) return DC_EINVAL;
   return replay_impl(c, rules, start, d_moves, n_games, n_plies, reinterpret_cast<u64*>(d_bitmap),
                      reinterpret_cast<u64*>(d_digests), stats);
@@ -827,7 +909,7 @@ int dc_replay_device(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint1
 
 int dc_replay(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* moves, uint32_t n_games,
               uint32_t n_plies, uint64_t* bitmap, uint64_t* digests, dc_replay_stats* stats) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (rules > DC_RULES_FIDE || (n_games && n_plies && !moves)) return DC_EINVAL;
   const size_t nm = (size_t)n_games * n_plies;
   const size_t words = (size_t)((n_games + 63) / 64) * n_plies;
@@ -848,7 +930,7 @@ int dc_replay(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* mo
 int dc_replay_info_device(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* d_moves, uint32_t n_games,
                           uint32_t n_plies, uint64_t* d_bitmap, uint64_t* d_digests, uint8_t* d_info,
                           dc_replay_stats* stats) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (rules > DC_RULES_FIDE || (n_games && n_plies && (!d_moves || !d_info))) return DC_EINVAL;
   return replay_impl(c, rules, start, d_moves, n_games, n_plies, reinterpret_cast<u64*>(d_bitmap),
                      reinterpret_cast<u64*>(d_digests), stats, d_info);
@@ -856,7 +938,7 @@ int dc_replay_info_device(dc_ctx* c, uint32_t rules, const dc_pos* start, const 
 
 int dc_replay_info(dc_ctx* c, uint32_t rules, const dc_pos* start, const uint16_t* moves, uint32_t n_games,
                    uint32_t n_plies, uint64_t* bitmap, uint64_t* digests, uint8_t* info, dc_replay_stats* stats) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (rules > DC_RULES_FIDE || (n_games && n_plies && (!moves || !info))) return DC_EINVAL;
   if (rules != DC_RULES_REF) return DC_EUNSUPPORTED;
   const size_t nm = (size_t)n_games * n_plies;
@@ -1048,13 +1130,13 @@ int dc_keccak256(const void* data, size_t len, uint8_t out[32]) {
 int dc_state_hash_device(dc_ctx* c, const dc_pos* start, const char* history, const char* d_names,
                          const uint32_t* d_names_off, const uint16_t* d_moves, uint32_t n_games, uint32_t n_plies,
                          uint8_t* d_hashes) {
-  ENTER(c);
+  ENTER_WORK(c);
   return state_hash_impl(c, start, history, d_names, d_names_off, d_moves, n_games, n_plies, d_hashes);
 }
 
 int dc_state_hash(dc_ctx* c, const dc_pos* start, const char* history, const char* names, const uint32_t* names_off,
                   const uint16_t* moves, uint32_t n_games, uint32_t n_plies, uint8_t* hashes) {
-  ENTER(c);
+  ENTER_WORK(c);
   if ((n_games && n_plies && !moves) || (n_games && !hashes)) return DC_EINVAL;
   const size_t nm = (size_t)n_games * n_plies;
   HIP_TRY(c->moves.ensure(std::max<size_t>(nm, 1)));
@@ -1102,7 +1184,7 @@ static int ensure_gtab(dc_ctx* c) {
 
 int dc_verify_tx_batch_device(dc_ctx* c, const char* d_strings, const uint32_t* d_str_off, const uint32_t* d_actions,
                               const int8_t* d_turns, uint32_t n, uint8_t* d_verdicts) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (n == 0) return DC_SUCCESS;
   if (!d_strings || !d_str_off || !d_actions || !d_verdicts) return DC_EINVAL;
   int e = ensure_gtab(c);
@@ -1115,7 +1197,7 @@ int dc_verify_tx_batch_device(dc_ctx* c, const char* d_strings, const uint32_t* 
 
 int dc_verify_tx_batch(dc_ctx* c, const char* strings, const uint32_t* str_off, const uint32_t* actions,
                        const int8_t* turns, uint32_t n, uint8_t* verdicts) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (n == 0) return DC_SUCCESS;
   if (!strings || !str_off || !actions || !verdicts) return DC_EINVAL;
   const size_t no = (size_t)4 * n + 1;
@@ -1140,7 +1222,7 @@ int dc_verify_tx_batch(dc_ctx* c, const char* strings, const uint32_t* str_off, 
 
 int dc_gen_games_device(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games,
                         uint32_t n_plies, uint32_t noise_per_256, uint16_t* d_out) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (rules > DC_RULES_FIDE || (n_games && n_plies && !d_out) || noise_per_256 > 256) return DC_EINVAL;
   if (!n_games || !n_plies) return DC_SUCCESS;
   HIP_TRY(c->timed("gen_games", (u64)n_games * n_plies, [&] {
@@ -1153,7 +1235,7 @@ int dc_gen_games_device(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first
 
 int dc_gen_games(dc_ctx* c, uint32_t rules, uint64_t seed, uint64_t first_game, uint32_t n_games, uint32_t n_plies,
                  uint32_t noise_per_256, uint16_t* out) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (rules > DC_RULES_FIDE || (n_games && n_plies && !out) || noise_per_256 > 256) return DC_EINVAL;
   const size_t nm = (size_t)n_games * n_plies;
   if (!nm) return DC_SUCCESS;
@@ -1664,13 +1746,13 @@ extern "C" {
 
 int dc_perft(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint64_t* divide, uint16_t* root_moves,
              uint32_t* n_root, uint64_t* total) {
-  ENTER(c);
+  ENTER_WORK(c);
   return perft_impl(c, rules, pos, depth, 1, 0, 1, divide, root_moves, n_root, total);
 }
 
 int dc_perft_shard(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
                    uint32_t n_shards, uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total) {
-  ENTER(c);
+  ENTER_WORK(c);
   return perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, divide, root_moves, n_root, total);
 }
 
@@ -1779,7 +1861,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
 
 int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
                            uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out) {
-  ENTER(c);
+  ENTER_WORK(c);
   if (!pos || (n_runs && !d_out) || rules > DC_RULES_FIDE || n_shards == 0 || shard >= n_shards || pos->stm > 1)
     return DC_EINVAL;
   if (depth < 2 || depth > 12) return DC_EUNSUPPORTED;
@@ -1791,7 +1873,7 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
 }
 
 int dc_ctx_synchronize(dc_ctx* c) {
-  ENTER(c);
+  ENTER_WORK(c);
   return sync_ctx(c);
 }
 

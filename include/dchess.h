@@ -173,9 +173,16 @@ int dc_apply_batch(dc_ctx* ctx, uint32_t rules, dc_pos* pos, const uint16_t* mov
  * its vote (core/src/consensus/hotstuff.rs:138, :52).  Results are identical
  * to the launched path.  The wave leaves after lease_us microseconds without a
  * call (at most 60 s; the next call restarts it), on dc_live_validator(ctx, 0)
- * and in dc_ctx_destroy.  While it is resident, a device-wide synchronisation
- * (hipDeviceSynchronize) of the same process waits for the lease to run out:
- * switch it off before one. */
+ * and in dc_ctx_destroy.  At most one wave is resident per process: a live
+ * call that starts its context's wave stops the others' first.  Every other
+ * call of this library that uses the device (perft, replay, hashing,
+ * signatures, launched validate / apply, device memory, dc_ctx_destroy) stops
+ * the resident wave first and keeps new ones from starting until it returns:
+ * HIP maps a process's streams onto a few hardware queues, and work queued
+ * behind a resident wave -- and hipFree, which waits for every stream -- would
+ * otherwise wait for its lease.  GPU work the CALLER issues itself (its own
+ * kernels, hipDeviceSynchronize, hipFree) while a wave is resident can wait
+ * for the lease: switch the validator off (lease 0) before such work. */
 int dc_live_validator(dc_ctx* ctx, uint32_t lease_us);
 
 /* ------------------------------------------------------------------ replay

@@ -136,3 +136,82 @@ def test_live_stamp_wrap(live):
             assert (live.validate_batch(pool_pos[idx], pool_mv[idx]) == pool_want[idx]).all(), k
         i = idx1[k:k + 1]
         assert live.validate_batch(pool_pos[i], pool_mv[i])[0] == pool_want[i[0]], k
+
+
+def test_live_waves_do_not_block_buffer_growth():
+    """hipFree / hipHostFree wait for every stream of the device, a resident
+    wave's too.  With a 20 s lease on this context and on a second
+    one, a perft that grows this context's buffers, a perft on the other
+    context, and a context destroyed beside them all finish far inside the
+    lease (every resident wave is stopped first, dc_api.hip LiveHold); the
+    live calls stay right afterwards."""
+    import json
+    import os
+    og = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))
+    d5 = og["perft_ref"]["startpos"]["5"]["total"]
+    pool_pos, pool_mv, pool_want = _pool(26)
+    rng = np.random.default_rng(26)
+    a, b = dchess.Engine(0), dchess.Engine(0)
+    try:
+        a.live_validator(20_000_000)
+        b.live_validator(20_000_000)
+        for e in (a, b):  # both waves resident
+            idx = rng.choice(len(pool_mv), 3, replace=False)
+            assert (e.validate_batch(pool_pos[idx], pool_mv[idx]) == pool_want[idx]).all()
+        steps = {}
+
+        def timed(name, f):
+            t0 = time.time()
+            r = f()
+            steps[name] = round(time.time() - t0, 3)
+            return r
+        assert timed("perft_a", lambda: a.perft(dchess.startpos(), 5))[0] == d5  # a's buffers grow
+        assert timed("perft_b", lambda: b.perft(dchess.startpos(), 5))[0] == d5
+        c = timed("create_c", lambda: dchess.Engine(0))
+        timed("perft_c", lambda: c.perft(dchess.startpos(), 3))
+        timed("close_c", c.close)
+        assert sum(steps.values()) < 5.0, steps
+        for e in (a, b, a):
+            idx = rng.choice(len(pool_mv), 9, replace=False)
+            assert (e.validate_batch(pool_pos[idx], pool_mv[idx]) == pool_want[idx]).all()
+    finally:
+        a.live_validator(0)
+        b.live_validator(0)
+        a.close()
+        b.close()
+
+
+def test_live_timeout_path_then_fresh_verdicts():
+    """A call whose answer does not come within the timeout returns DC_EHIP;
+    its request is cleared and its stamp burnt, so the next call is never
+    answered with the timed-out request's verdict.  The timeout is
+    shortened through the test hook dc_test_live_timeout."""
+    import ctypes as C
+    L = dchess.lib()
+    L.dc_test_live_timeout.argtypes = [C.c_void_p, C.c_uint32]
+    pool_pos, pool_mv, pool_want = _pool(27)
+    ok = np.nonzero(pool_want == 0)[0]
+    bad = np.nonzero(pool_want == 3)[0]
+    e = dchess.Engine(0)
+    try:
+        e.live_validator(200_000)
+        timeouts = 0
+        for k in range(200):
+            L.dc_test_live_timeout(e.ctx, 0)
+            i = ok[k % len(ok):k % len(ok) + 1]
+            out = np.zeros(1, np.uint8)
+            pp = np.ascontiguousarray(pool_pos[i])
+            mv = np.ascontiguousarray(pool_mv[i])
+            r = L.dc_validate_batch(e.ctx, 0, pp.ctypes.data, mv.ctypes.data, 1, out.ctypes.data)
+            L.dc_test_live_timeout(e.ctx, 5_000_000)
+            if r != 0:
+                timeouts += 1
+                j = bad[k % len(bad):k % len(bad) + 1]  # a verdict the timed-out request cannot give
+                assert e.validate_batch(pool_pos[j], pool_mv[j])[0] == 3
+                assert e.validate_batch(pool_pos[i], pool_mv[i])[0] == 0
+            else:
+                assert out[0] == 0
+        assert timeouts > 0
+    finally:
+        e.live_validator(0)
+        e.close()

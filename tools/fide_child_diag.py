@@ -23,6 +23,7 @@ import ctypes as C
 import json
 import os
 import sys
+import time
 from collections import Counter
 
 import numpy as np
@@ -58,7 +59,13 @@ def main():
     ap.add_argument("--save-map")
     ap.add_argument("--kmap")
     ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--noise", type=int, default=-1, help="co-resident noise kind (tools/diag/noise.hip)")
+    ap.add_argument("--noise-blocks", type=int, default=512)
     args = ap.parse_args()
+    noise = None
+    if args.noise >= 0:
+        noise = C.CDLL(os.path.join(REPO, "tools", "diag", "libnoise.so"))
+        noise.noise_start.argtypes = [C.c_int, C.c_int, C.c_double]
     names = args.names
     og = json.load(open(os.path.join(REPO, "tests", "golden", "oracle_golden.json")))["perft_fide"]
     eng = dchess.Engine(0)
@@ -73,8 +80,16 @@ def main():
         buf.fill_(-1)
         torch.cuda.synchronize()
         assert L.dc_diag_child_set(buf.data_ptr(), cap) == 0
+        if noise is not None:
+            eng.perft(dchess.pos_from_fen(og[name]["fen"]), args.depth, rules=dchess.RULES_FIDE)  # capture first
+            buf.fill_(-1)
+            torch.cuda.synchronize()
+            assert noise.noise_start(args.noise, args.noise_blocks, 1500.0) == 0
+            time.sleep(0.05)
         tot = eng.perft(dchess.pos_from_fen(og[name]["fen"]), args.depth, rules=dchess.RULES_FIDE)[0]
         torch.cuda.synchronize()
+        if noise is not None:
+            assert noise.noise_wait() == 0
         assert L.dc_diag_child_set(None, 0) == 0
         pub = og[name]["perft"][str(args.depth)]
         if args.kmap:
