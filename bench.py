@@ -683,6 +683,45 @@ _OG = json.load(open(os.path.join(REPO, "tests", "golden", "oracle_golden.json")
 FIDE_SUITE = ("startpos", "kiwipete", "pos3", "pos4", "pos5", "pos6")
 
 
+def concurrent_perfts(d, args, items, depth, steps, rules):
+    """The positions of a suite timed as one batch: one context -- one stream
+    -- per position, every position's `steps` repeat runs enqueued before any
+    is waited for, so the small per-position launch sequences (a depth-5 FIDE
+    final stage has 3k-100k parents) fill the GPU together instead of one
+    after another.  Returns (leaves, wall seconds); every step of every
+    position is checked against its published count after the timed region."""
+    W = 258
+    engs, bufs = [], []
+    for pos, want in items:
+        e = dchess.Engine(d.device)
+        engs.append(e)
+        tot, _, _ = e.perft(pos, depth, rules=rules)  # warm-up, parity
+        if tot != want:
+            raise SystemExit(f"parity failure: FIDE perft({depth}) = {tot}, expected {want}")
+        nw = REPEAT_BATCH if steps >= REPEAT_BATCH else 1
+        b = e.alloc(max(nw, steps) * W * 8)
+        e.perft_repeat_device(pos, depth, args.split, 0, 1, nw, b, rules=rules)  # graph captures
+        e.synchronize()
+        bufs.append(b)
+    d.sync()
+    t0 = time.perf_counter()
+    for (pos, _), e, b in zip(items, engs, bufs):
+        e.perft_repeat_device(pos, depth, args.split, 0, 1, steps, b, rules=rules)
+    for e in engs:
+        e.synchronize()
+    d.sync()
+    dt = time.perf_counter() - t0
+    leaves = 0
+    for (pos, want), e, b in zip(items, engs, bufs):
+        res = b.download(np.uint64, steps * W).reshape(steps, W)
+        if not (res[:, 257] == want).all():
+            raise SystemExit(f"parity failure in a concurrent FIDE step: {res[:, 257][:4]} != {want}")
+        leaves += want * steps
+        b.free()
+        e.close()
+    return leaves, dt
+
+
 def fide_leg(eng, d, args, name, depth, keys, pmc_key):
     """FIDE perft (DC_RULES_FIDE: castling, en passant, promotion, no self-check)
     of one or more positions, each timed like the headline (dc_perft_repeat_device
@@ -700,6 +739,11 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
         leaves += lv
         dt += t
         per[k] = {"leaves": want, "ms_per_step": 1e3 * t / steps}
+    seq_ms = 1e3 * dt / steps
+    batched = len(keys) > 1 and d.dist is None
+    if batched:  # the suite as one batch (concurrent streams): the leg's value
+        items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in keys]
+        leaves, dt = concurrent_perfts(d, args, items, depth, steps, dchess.RULES_FIDE)
         eng.reset_stats()
         eng.set_profiling(True)
         perft_step(eng, d, args, pos, depth, dchess.RULES_FIDE)
@@ -713,6 +757,11 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
            "workload": name, "rules": "FIDE", "scaling": "strong", "leaves_per_step": leaves // steps,
            "parity": "published tables (chessprogramming wiki), every timed step", "positions": per,
            "final_kernel_ms": kms}
+    if batched:
+        out["batch"] = ("the positions as one batch: one context (stream) per position, every position's "
+                        "repeat runs enqueued before any wait; positions[].ms_per_step and sequential_ms_per_step "
+                        "time them one after another")
+        out["sequential_ms_per_step"] = seq_ms
     rec = _pmc(pmc_key) if d.world == 1 else None
     if rec and kl and kms > 0:
         out["roofline"] = valu_roof("k_count2b", kunits / (kms / 1e3), "leaf", W_COUNT2, rec,

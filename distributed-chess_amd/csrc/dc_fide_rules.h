@@ -168,11 +168,14 @@ struct Analysis {
 // store through a selected address (&a.checkers or &a.pinned), which kept the
 // whole Analysis in scratch memory (round 3: 536 B/lane in k_count2b<Fide>).
 // Two unconditional value updates keep both in registers.
+// kup / kdn: the squares above / below the king (above_mask / below_mask),
+// made once by analyse before its gates.
 template <int STM, int D>
-__device__ __forceinline__ void scan_dir(const FPos<STM>& f, int ksq, const Lines& l, u64& checkers, u64& pinned) {
+__device__ __forceinline__ void scan_dir(const FPos<STM>& f, u64 kup, u64 kdn, const Lines& l, u64& checkers,
+                                         u64& pinned) {
   constexpr bool UP = (D & 1) == 0;  // 0 N, 2 E, 4 NE, 6 NW go to higher squares
   const u64 line = (D < 2) ? l.file : (D < 4) ? l.rank : (D < 6) ? l.diag : l.anti;
-  const u64 ray = line & (UP ? above_mask(ksq) : below_mask(ksq));
+  const u64 ray = line & (UP ? kup : kdn);
   const u64 sl = (D < 4) ? f.tO : f.tD;
   const u64 blk = f.occ & ray;
   // first and second occupied squares on the ray (bits; 0 when absent)
@@ -209,24 +212,32 @@ __device__ __forceinline__ Analysis analyse(const FPos<STM>& f, bool with_danger
   if (a.ksq < 0) return a;
   a.checkers = (pawn_attacks<STM>(f.K) & f.tP) | (knight_attacks(f.K) & f.tN);
   const Lines l = lines_of(a.ksq);
+  // The king's half-line masks are made here, before the line gates, and kept
+  // opaque.  Left to the compiler they were made between a gate's 64-bit
+  // compare and its branch, the second shift overwriting the compare's
+  // operands: the three-instruction window in which a co-resident wave's
+  // single-issue VALU instruction made the round-4 table variant miscount
+  // (tools/vccz_check.py --shape).
+  u64 kup = above_mask(a.ksq), kdn = below_mask(a.ksq);
+  asm volatile("" : "+v"(kup), "+v"(kdn));
   u64 chk = a.checkers, pin = 0;
 #if DC_FIDE_SNIPER == 2
   // (diagnostics) the same gate as a per-lane branch (no __ballot)
   if ((l.file & f.tO) != 0) {
-    scan_dir<STM, 0>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 1>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 0>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 1>(f, kup, kdn, l, chk, pin);
   }
   if ((l.rank & f.tO) != 0) {
-    scan_dir<STM, 2>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 3>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 2>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 3>(f, kup, kdn, l, chk, pin);
   }
   if ((l.diag & f.tD) != 0) {
-    scan_dir<STM, 4>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 5>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 4>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 5>(f, kup, kdn, l, chk, pin);
   }
   if ((l.anti & f.tD) != 0) {
-    scan_dir<STM, 6>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 7>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 6>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 7>(f, kup, kdn, l, chk, pin);
   }
 #elif DC_FIDE_SNIPER
   // a line through the king with no enemy slider of its kind on it can hold
@@ -234,30 +245,30 @@ __device__ __forceinline__ Analysis analyse(const FPos<STM>& f, bool with_danger
   // skips that line's two scans (round 4: the eight scans were ~19 % of the
   // FIDE final stage, tools/bbprof_inline.py)
   if (__ballot((l.file & f.tO) != 0)) {
-    scan_dir<STM, 0>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 1>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 0>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 1>(f, kup, kdn, l, chk, pin);
   }
   if (__ballot((l.rank & f.tO) != 0)) {
-    scan_dir<STM, 2>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 3>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 2>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 3>(f, kup, kdn, l, chk, pin);
   }
   if (__ballot((l.diag & f.tD) != 0)) {
-    scan_dir<STM, 4>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 5>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 4>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 5>(f, kup, kdn, l, chk, pin);
   }
   if (__ballot((l.anti & f.tD) != 0)) {
-    scan_dir<STM, 6>(f, a.ksq, l, chk, pin);
-    scan_dir<STM, 7>(f, a.ksq, l, chk, pin);
+    scan_dir<STM, 6>(f, kup, kdn, l, chk, pin);
+    scan_dir<STM, 7>(f, kup, kdn, l, chk, pin);
   }
 #else
-  scan_dir<STM, 0>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 1>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 2>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 3>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 4>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 5>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 6>(f, a.ksq, l, chk, pin);
-  scan_dir<STM, 7>(f, a.ksq, l, chk, pin);
+  scan_dir<STM, 0>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 1>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 2>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 3>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 4>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 5>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 6>(f, kup, kdn, l, chk, pin);
+  scan_dir<STM, 7>(f, kup, kdn, l, chk, pin);
 #endif
   a.checkers = chk;
   a.pinned = pin;
