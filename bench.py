@@ -743,6 +743,7 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
     batched = len(keys) > 1 and d.dist is None
     if batched:  # the suite as one batch (concurrent streams): the leg's value
         items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in keys]
+        steps = max(16, args.steps)  # a step is ~0.5 ms: enough steps for the 8-run batch graphs
         leaves, dt = concurrent_perfts(d, args, items, depth, steps, dchess.RULES_FIDE)
         eng.reset_stats()
         eng.set_profiling(True)

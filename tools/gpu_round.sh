@@ -14,7 +14,7 @@ step() { echo "[$(date +%T)] $*" >> $O/steps.log; }
 mkdir -p $O
 if has test; then
   step pytest
-  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+  timeout -k 10 1200 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
   tail -2 $O/pytest_gpu.log
 fi
 if has bench; then
