@@ -932,16 +932,27 @@ struct C2bCfg {
   static constexpr u32 kCap = SPLIT ? 256 * 22 : 256 * 28;  // child slots per window
 };
 
+// The per-parent sensitivity sets exist in the split instantiation only (the
+// REF-shaped one carries no 2 KB of dead LDS).
 template <bool SPLIT>
-struct C2bShared {
+struct C2bSens {
+  u64 sens[SN_COUNT][256];  // sens_masks, [set][parent]
+};
+template <>
+struct C2bSens<false> {};
+
+template <bool SPLIT>
+struct C2bShared : C2bSens<SPLIT> {
   Board par[256];
   u32 pmeta[256];
   u32 slot[C2bCfg<SPLIT>::kCap];
   u64 hist[256];
   u64 wsum[4];
   uint16_t ptag[256];
-  u64 sens[SPLIT ? SN_COUNT : 1][256];  // sens_masks, [set][parent]
 };
+static_assert(sizeof(C2bShared<false>) + sizeof(u64) * SN_COUNT * 256 == sizeof(C2bShared<true>) +
+                  sizeof(u32) * (C2bCfg<false>::kCap - C2bCfg<true>::kCap),
+              "only the split instantiation carries the sensitivity sets");
 
 // DC_DIAG_CHILD (diagnostic builds only, never the product):
 // every child k_count2b counts is written as one 64-byte record at a position
@@ -998,7 +1009,8 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
     u64 simple_leaves = 0;  // simple children x c0 (SPLIT)
     // the lane's sensitivity sets, read from LDS where the enumeration uses
     // them (the thread index rebuilt at each use, otid: no address kept live)
-    auto sens_at = [&](int k) -> u64 { return sh.sens[k][otid(wave)]; };
+    // (generic: its body is instantiated only where the split calls it)
+    auto sens_at = [&](auto k) -> u64 { return sh.sens[k][otid(wave)]; };
     if constexpr (SPLIT) {
       if (valid) {
         u64 m[SN_COUNT];
@@ -1378,7 +1390,6 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
 #endif
   };
   auto consume = [&](const Cand& c, bool live) {
-    const u32 pl = c.e >> 15;
     const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
     const u64 occ = occupied(c.pb);
     const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
