@@ -1348,7 +1348,7 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       Fs = ps.Fs;
       Ts = ps.Ts;
       cnt = ps.n_total - ps.n_simple;  // enumerated (special) children only
-      simple_leaves = (u64)ps.n_simple * (ps.base + ps.pawn_o);
+      simple_leaves = (u32)(ps.n_simple * (ps.base + ps.pawn_o) + ps.gcorr);  // (>= 0: a sum of child counts)
       nsim = ps.n_simple;
     } else {
       cnt = ref_count<STM>(p);
@@ -1492,9 +1492,16 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
       if constexpr (GQ) {
         const Board pp = sh.board(otid(w));
         u32 unused;
-        const u64 keep = ~(sh.rays(otid(w)) | ref_pawn_sensitive<1 - STM>(pp, unused));
+        const u64 rays = sh.rays(otid(w));
         const u64 occ = occupied(pp), own = STM ? pp.b0 : (occ & ~pp.b0);
+#if DC_C2C_GCORR
+        u64 p1, n1, big;
+        const u64 g = ref_pawn_planes<1 - STM>(pp, unused, p1, n1, big);
+        ref_for_each_special<STM>(pp, own & ~(rays | g), ~(occ | rays | big), visit);
+#else
+        const u64 keep = ~(rays | ref_pawn_sensitive<1 - STM>(pp, unused));
         ref_for_each_special<STM>(pp, own & keep, ~occ & keep, visit);
+#endif
       } else if constexpr (BULK) {
         ref_for_each_special<STM>(p, Fs, Ts, visit);
       } else {

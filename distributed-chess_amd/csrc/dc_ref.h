@@ -403,6 +403,33 @@ __device__ __forceinline__ u64 ref_pawn_sensitive(const Board& b, u32& pawn_cnt)
   return bop3<0xFE>(q1, cw, ce) | land;
 }
 
+// ref_pawn_sensitive plus the weight planes of g on the parent (DC_C2C_GCORR):
+//   g(x) = [x in cw] + [x in ce] - [x in q1] - [x in mid] - [x in land]
+// (cw/ce: SIDE's pawn capture squares, q1: its push squares, mid: middle
+// squares of a double push whose landing is empty, land: landings whose
+// middle is empty).  For a quiet move f -> t of the other side with f off G
+// and t empty, SIDE's pawn-move count in the child is pawn_cnt + g(t)
+// (tools/ref_gsplit_proto.py: 0 mismatches against the oracle).  P1 / N1: the
+// squares where g = +1 / -1; BIG: |g| = 2 (rare; such targets stay enumerated).
+template <int SIDE>
+__device__ __forceinline__ u64 ref_pawn_planes(const Board& b, u32& pawn_cnt, u64& P1, u64& N1, u64& BIG) {
+  typedef PawnDir<SIDE> PD;
+  const Sides s = sides<SIDE>(b);
+  const u64 q1 = sh<PD::F>(s.P);
+  const u64 cw = sh<PD::CW>(s.P) & kNotH, ce = sh<PD::CE>(s.P) & kNotA;
+  const u64 push1 = q1 & s.empty;
+  const u64 land = sh<PD::F>(push1) & PD::ROW_DBL;  // landings whose mid is empty
+  pawn_cnt = pc(or_and(push1, land, s.empty)) + pc(cw & s.enemy) + pc(ce & s.enemy);
+  const u64 mid = and3(q1, PD::ROW_AFTER1, sh<-PD::F>(s.empty & PD::ROW_DBL));  // mids whose landing is empty
+  const u64 nd = mid | land;  // disjoint rows; mid is inside q1
+  const u64 s1 = cw ^ ce, s2 = cw & ce, n1 = q1 ^ nd, n2 = q1 & nd;  // g = (s1 + 2 s2) - (n1 + 2 n2)
+  const u64 sp = s1 | s2, sn = n1 | n2;
+  P1 = (s2 & n1) | (s1 & ~sn);
+  N1 = (n2 & s1) | (n1 & ~sp);
+  BIG = (s2 & ~sn) | (n2 & ~sp);
+  return bop3<0xFE>(q1, cw, ce) | land;
+}
+
 // Moves of STM in `b` with source in Fs and target in Ts ("simple" moves;
 // Ts holds empty squares only, so pawn captures never count): ref_count<STM>
 // with the sources and targets restricted.  Slider targets of sources in Fs
@@ -456,7 +483,18 @@ __device__ __forceinline__ void ray_attacks2(u64 g1, u64 g2, u64 empty, u64& r1,
 struct ParentSplit {
   u64 att, Fs, Ts, orth;
   u32 base, pawn_o, n_total, n_simple, diag;
+  u32 gcorr;  // (GCORR) sum of g(t) over the simple moves, mod 2^32 (may be negative)
 };
+
+// GCORR (round 5): a quiet move with f off att and G and t off att (and off
+// BIG) is simple too, its child's count corrected by g(t) (ref_pawn_planes):
+// Ts = empty & ~(att | BIG) instead of empty & ~(att | G), and each class's
+// simple targets are also counted on the g = +1 and g = -1 planes.  80 % of
+// the quiet children round 4 enumerated for a pawn recount become simple
+// (tools/ref_gsplit_proto.py).
+#ifndef DC_C2C_GCORR
+#define DC_C2C_GCORR 1
+#endif
 
 // GROUPS: also orth/diag (ref_count_nonpawn_g) for the group-wise recount.
 // TGT: also the side to move's slider target sets per direction (tgt[0..7]
@@ -466,9 +504,22 @@ template <int STM, bool GROUPS = false, bool TGT = false>
 __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r, u64* tgt = nullptr) {
   if constexpr (GROUPS) r.base = ref_count_nonpawn_g<1 - STM>(b, r.att, r.orth, r.diag);
   else r.base = ref_count_nonpawn<1 - STM>(b, r.att);
-  const u64 keep = ~(r.att | ref_pawn_sensitive<1 - STM>(b, r.pawn_o));
   const Sides s = sides<STM>(b);
+#if DC_C2C_GCORR
+  u64 P1, N1, BIG;
+  const u64 Fs = s.own & ~(r.att | ref_pawn_planes<1 - STM>(b, r.pawn_o, P1, N1, BIG));
+  const u64 Ts = s.empty & ~(r.att | BIG), no = s.notown;
+  u32 gp = 0, gn = 0;
+  // a class's simple targets X on the two weight planes
+  auto wgt = [&](u64 x) {
+    gp += pc(x & P1);
+    gn += pc(x & N1);
+  };
+#else
+  const u64 keep = ~(r.att | ref_pawn_sensitive<1 - STM>(b, r.pawn_o));
   const u64 Fs = s.own & keep, Ts = s.empty & keep, no = s.notown;
+  auto wgt = [](u64) {};
+#endif
   r.Fs = Fs;
   r.Ts = Ts;
   u64 e = s.empty;
@@ -477,7 +528,9 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   const u64 push1 = sh<PD::F>(s.P) & e, push1s = sh<PD::F>(s.P & Fs) & e;
   // single and double pushes land on disjoint squares: one popcount each
   u32 t = pc(or_and(push1, sh<PD::F>(push1) & PD::ROW_DBL, e));
-  u32 m = pc(bop3<0xA8>(push1s, sh<PD::F>(push1s) & PD::ROW_DBL, Ts));  // (a | b) & c
+  const u64 pm = bop3<0xA8>(push1s, sh<PD::F>(push1s) & PD::ROW_DBL, Ts);  // (a | b) & c
+  u32 m = pc(pm);
+  wgt(pm);
   t += pc(and3(sh<PD::CW>(s.P), kNotH, s.enemy)) + pc(and3(sh<PD::CE>(s.P), kNotA, s.enemy));
   using std::integral_constant;
 #if DC_KNIGHT_TAB
@@ -486,14 +539,18 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
     const int f = lsb(n) & 63;
     const u64 a = kAtt.knight[f];
     t += pc(a & no);
-    m += ((Fs >> f) & 1) ? pc(a & Ts) : 0u;
+    const u64 x = ((Fs >> f) & 1) ? a & Ts : 0ull;
+    m += pc(x);
+    wgt(x);
   }
 #else
   const u64 n = s.N, ns = s.N & Fs;
   auto leap = [&](auto dtag, u64 guard) {
     constexpr int D = decltype(dtag)::value;
     t += pc(and3(sh<D>(n), guard, no));
-    m += pc(and3(sh<D>(ns), guard, Ts));
+    const u64 x = and3(sh<D>(ns), guard, Ts);
+    m += pc(x);
+    wgt(x);
   };
   leap(integral_constant<int, 17>{}, kNotA);
   leap(integral_constant<int, 15>{}, kNotH);
@@ -507,10 +564,15 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   if (DC_ATT_TAB && (s.K & (s.K - 1)) == 0) {  // one king (or none): one attack set for both counts
     const u64 ka = s.K ? kAtt.king[lsb(s.K) & 63] : 0ull;
     t += pc(ka & no);
-    m += (s.K & Fs) ? pc(ka & Ts) : 0u;
+    const u64 x = (s.K & Fs) ? ka & Ts : 0ull;
+    m += pc(x);
+    wgt(x);
   } else {
     t += king_moves(s.K, no);
     m += king_moves(s.K & Fs, Ts);
+#if DC_C2C_GCORR
+    for (u64 k = s.K & Fs; k; k &= k - 1) wgt(king_att_sq(lsb(k)) & Ts);  // several kings (cells adapter)
+#endif
   }
 #ifndef DC_C2C_KSKIP
 #define DC_C2C_KSKIP 1
@@ -532,6 +594,7 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
     const u64 rt = ra & no, st = rs & Ts;
     t += pc(rt);
     m += pc(st);
+    wgt(st);
     // (TGT) the special targets only: t in Ts is simple iff its source is
     // in Fs, i.e. iff t is in the fill from the sliders in Fs (rs)
     if constexpr (TGT) tgt[decltype(itag)::value] = and_andn(ra, no, st);
@@ -559,6 +622,11 @@ __device__ __forceinline__ void ref_parent_split(const Board& b, ParentSplit& r,
   else diag(T1{});
   r.n_total = t;
   r.n_simple = m;
+#if DC_C2C_GCORR
+  r.gcorr = gp - gn;
+#else
+  r.gcorr = 0;
+#endif
 }
 
 // The knight and king moves of ref_for_each_special(_pre), in one order both
