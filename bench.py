@@ -698,11 +698,15 @@ def concurrent_perfts(d, args, items, depth, steps, rules):
         tot, _, _ = e.perft(pos, depth, rules=rules)  # warm-up, parity
         if tot != want:
             raise SystemExit(f"parity failure: FIDE perft({depth}) = {tot}, expected {want}")
-        nw = REPEAT_BATCH if steps >= REPEAT_BATCH else 1
-        b = e.alloc(max(nw, steps) * W * 8)
-        e.perft_repeat_device(pos, depth, args.split, 0, 1, nw, b, rules=rules)  # graph captures
+        b = e.alloc(max(REPEAT_BATCH, steps) * W * 8)
+        for nw in (1, REPEAT_BATCH):  # graph captures (the one-run and the batch graph)
+            e.perft_repeat_device(pos, depth, args.split, 0, 1, nw, b, rules=rules)
         e.synchronize()
         bufs.append(b)
+    for (pos, _), e, b in zip(items, engs, bufs):  # one untimed concurrent pass
+        e.perft_repeat_device(pos, depth, args.split, 0, 1, steps, b, rules=rules)
+    for e in engs:
+        e.synchronize()
     d.sync()
     t0 = time.perf_counter()
     for (pos, _), e, b in zip(items, engs, bufs):
@@ -739,12 +743,7 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
         leaves += lv
         dt += t
         per[k] = {"leaves": want, "ms_per_step": 1e3 * t / steps}
-    seq_ms = 1e3 * dt / steps
-    batched = len(keys) > 1 and d.dist is None
-    if batched:  # the suite as one batch (concurrent streams): the leg's value
-        items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in keys]
-        steps = max(16, args.steps)  # a step is ~0.5 ms: enough steps for the 8-run batch graphs
-        leaves, dt = concurrent_perfts(d, args, items, depth, steps, dchess.RULES_FIDE)
+        # the final stage's kernel time of one step (profiled run, outside the timed region)
         eng.reset_stats()
         eng.set_profiling(True)
         perft_step(eng, d, args, pos, depth, dchess.RULES_FIDE)
@@ -754,6 +753,17 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
         kms += ks["total_ms"]
         kl += ks["launches"]
         kunits += want // d.world
+    seq_ms = 1e3 * dt / steps
+    batched = len(keys) > 1 and d.dist is None
+    if batched:  # the suite as one batch (concurrent streams): the leg's value
+        # longest first (the sequential times above): with more streams than hardware
+        # queues (GPU_MAX_HW_QUEUES), a queue shared by two streams pairs a long
+        # position with a short one
+        order = sorted(keys, key=lambda k: -per[k]["ms_per_step"])
+        items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in order]
+        # a step is ~0.5 ms: whole 8-run batch graphs, at least two per position
+        steps = REPEAT_BATCH * max(2, -(-args.steps // REPEAT_BATCH))
+        leaves, dt = concurrent_perfts(d, args, items, depth, steps, dchess.RULES_FIDE)
     out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
            "workload": name, "rules": "FIDE", "scaling": "strong", "leaves_per_step": leaves // steps,
            "parity": "published tables (chessprogramming wiki), every timed step", "positions": per,

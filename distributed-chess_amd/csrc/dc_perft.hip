@@ -1009,8 +1009,10 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
     u64 simple_leaves = 0;  // simple children x c0 (SPLIT)
     // the lane's sensitivity sets, read from LDS where the enumeration uses
     // them (the thread index rebuilt at each use, otid: no address kept live)
-    // (generic: its body is instantiated only where the split calls it)
-    auto sens_at = [&](auto k) -> u64 { return sh.sens[k][otid(wave)]; };
+    auto sens_at = [&](int k) -> u64 {
+      if constexpr (SPLIT) return sh.sens[k][otid(wave)];  // (the sets exist in the split only)
+      else return 0ull;
+    };
     if constexpr (SPLIT) {
       if (valid) {
         u64 m[SN_COUNT];
