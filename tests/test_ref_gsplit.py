@@ -19,5 +19,7 @@ import ref_gsplit_proto as R  # noqa: E402
 def test_target_side_correction_identity():
     st = R.check(1500, seed=7)
     assert st["mismatches"] == 0, st
+    # the source-side extension (pawn/knight/king sources on G; not in the kernel)
+    assert st["src_mismatches"] == 0 and st["src_bulk"] > 0, st
     # the correction moves most of round 4's enumerated quiet children into the bulk
     assert st["quiet_special_new"] < 0.5 * st["quiet_special_old"], st

@@ -92,7 +92,8 @@ def planes(pos):
     P1 = sum(1 << s for s in range(64) if g[s] == 1)
     N1 = sum(1 << s for s in range(64) if g[s] == -1)
     big = sum(1 << s for s in range(64) if abs(g[s]) >= 2)
-    return dict(att=att, G=G, P1=P1, N1=N1, big=big, g=g, occ=occ, ownO=ownO)
+    mids = q1 & row_mid  # middle squares of O double pushes (an O pawn on its start row behind)
+    return dict(att=att, G=G, P1=P1, N1=N1, big=big, g=g, occ=occ, ownO=ownO, mids=mids, F=F)
 
 
 def count_o(pos):
@@ -109,7 +110,7 @@ def check(n, seed=3):
     # startpos and the REF d6 goldens' boards (mid-game, kingless, unknown-kind, two kings)
     roots = [O.Pos()] + [O.Pos(np.array(e["cells"], np.int8), e["stm"], 0, -1) for e in d6.values()]
     st = dict(positions=0, children=0, simple_old=0, bulk_new=0, quiet_special_old=0, quiet_special_new=0,
-              big_targets=0, mismatches=0)
+              big_targets=0, mismatches=0, src_bulk=0, src_mismatches=0, quiet_special_src=0)
     for i in range(n):
         pos = roots[0 if i % 2 else rng.randrange(len(roots))].copy()
         for _ in range(rng.choice([5, 5, 5, 9, 15, 25]) if i % 2 else rng.randrange(0, 6)):
@@ -138,6 +139,23 @@ def check(n, seed=3):
             st["quiet_special_old"] += not old_simple
             st["quiet_special_new"] += not new_bulk
             st["big_targets"] += bool(not (G >> f & 1) and pl["big"] >> t & 1)
+            # source side (round 5b): a pawn, knight or king on G (off BIG) moving quietly to t off BIG:
+            # count_O = base + pawn_O + g(t) - g(f) + I, I = -1 when f, t are the mid and landing
+            # squares of one O double push
+            kind = int(pos.cells[f]) & 7
+            src_bulk = (G >> f & 1) and not (pl["big"] >> f & 1) and not (pl["big"] >> t & 1) and kind in (P_, N_, K_)
+            if src_bulk:
+                mids, F = pl["mids"], pl["F"]
+                pair = (mids >> f & 1 and t == f + F) or (mids >> t & 1 and f == t + F)
+                want = len(O.fast_gen_moves(O.fast_make(pos, m, O.REF), O.REF))
+                got = base_pawn + pl["g"][t] - pl["g"][f] - (1 if pair else 0)
+                st["src_bulk"] += 1
+                if want != got:
+                    st["src_mismatches"] += 1
+                    if st["src_mismatches"] < 5:
+                        print("src mismatch", pos.cells.tolist(), pos.stm, f, t, want, got, file=sys.stderr)
+            elif not new_bulk:
+                st["quiet_special_src"] += 1
             if new_bulk:
                 want = len(O.fast_gen_moves(O.fast_make(pos, m, O.REF), O.REF))  # O to move in the child
                 got = base_pawn + pl["g"][t]
