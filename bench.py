@@ -726,6 +726,46 @@ def concurrent_perfts(d, args, items, depth, steps, rules):
     return leaves, dt
 
 
+def batch_perfts(eng, d, args, items, depth, steps, rules):
+    """The positions of a suite as ONE tree (dc_perft_batch_repeat_device: same side
+    to move, root moves sharing the divide tags), so every level and the final
+    stage run one grid over all positions.  Returns (leaves, wall seconds,
+    final-stage kernel ms of one profiled batch run); every step's per-position
+    totals (divide summed over dc_perft_batch's root_pos) are checked against the
+    published counts after the timed region."""
+    W = 258
+    pos = [p for p, _ in items]
+    want = [w for _, w in items]
+    tot, div, rm, rp = eng.perft_batch(pos, depth, rules=rules)  # warm-up, parity, the root-move owners
+    if [int(x) for x in tot] != want:
+        raise SystemExit(f"parity failure: batch FIDE perft({depth}) = {list(tot)}, expected {want}")
+    b = eng.alloc(max(REPEAT_BATCH, steps) * W * 8)
+    for nw in (1, REPEAT_BATCH):  # graph captures (the one-run and the batch graph)
+        eng.perft_batch_repeat_device(pos, depth, args.split, nw, b, rules=rules)
+    eng.perft_batch_repeat_device(pos, depth, args.split, steps, b, rules=rules)  # one untimed pass
+    eng.synchronize()
+    d.sync()
+    t0 = time.perf_counter()
+    eng.perft_batch_repeat_device(pos, depth, args.split, steps, b, rules=rules)
+    eng.synchronize()
+    d.sync()
+    dt = time.perf_counter() - t0
+    res = b.download(np.uint64, steps * W).reshape(steps, W)
+    b.free()
+    nr = len(rp)
+    for r in range(steps):
+        per = [int(res[r, :nr][rp == i].sum()) for i in range(len(pos))]
+        if per != want:
+            raise SystemExit(f"parity failure in a batch FIDE step: {per} != {want}")
+    eng.reset_stats()
+    eng.set_profiling(True)
+    eng.perft_batch(pos, depth, rules=rules)
+    d.sync()
+    eng.set_profiling(False)
+    ks = eng.kernel_stats("count2")
+    return sum(want) * steps, dt, ks["total_ms"], ks["launches"]
+
+
 def fide_leg(eng, d, args, name, depth, keys, pmc_key):
     """FIDE perft (DC_RULES_FIDE: castling, en passant, promotion, no self-check)
     of one or more positions, each timed like the headline (dc_perft_repeat_device
@@ -755,23 +795,34 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
         kunits += want // d.world
     seq_ms = 1e3 * dt / steps
     batched = len(keys) > 1 and d.dist is None
-    if batched:  # the suite as one batch (concurrent streams): the leg's value
-        # longest first (the sequential times above): with more streams than hardware
-        # queues (GPU_MAX_HW_QUEUES), a queue shared by two streams pairs a long
-        # position with a short one
-        order = sorted(keys, key=lambda k: -per[k]["ms_per_step"])
-        items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in order]
-        # a step is ~0.5 ms: whole 8-run batch graphs, at least two per position
+    how = None
+    if batched:  # the suite as one batch: the leg's value
+        items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in keys]
+        # whole 8-run batch graphs, at least two
         steps = REPEAT_BATCH * max(2, -(-args.steps // REPEAT_BATCH))
-        leaves, dt = concurrent_perfts(d, args, items, depth, steps, dchess.RULES_FIDE)
+        try:  # one tree (dc_perft_batch): one launch sequence for all positions
+            leaves, dt, bkms, bkl = batch_perfts(eng, d, args, items, depth, steps, dchess.RULES_FIDE)
+            how = "tree"
+            kms, kl = bkms, bkl  # the roofline's kernel: the batch's one final stage
+        except dchess.DChessError:  # (more than 256 root moves, or mixed sides to move)
+            # one context (stream) per position, longest first (the sequential times
+            # above): with more streams than hardware queues (GPU_MAX_HW_QUEUES), a
+            # queue shared by two streams pairs a long position with a short one
+            order = sorted(keys, key=lambda k: -per[k]["ms_per_step"])
+            items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in order]
+            leaves, dt = concurrent_perfts(d, args, items, depth, steps, dchess.RULES_FIDE)
+            how = "streams"
     out = {"value": leaves / dt, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt / steps, "steps": steps,
            "workload": name, "rules": "FIDE", "scaling": "strong", "leaves_per_step": leaves // steps,
            "parity": "published tables (chessprogramming wiki), every timed step", "positions": per,
            "final_kernel_ms": kms}
     if batched:
-        out["batch"] = ("the positions as one batch: one context (stream) per position, every position's "
-                        "repeat runs enqueued before any wait; positions[].ms_per_step and sequential_ms_per_step "
-                        "time them one after another")
+        out["batch"] = ({"tree": "the positions as one tree (dc_perft_batch_repeat_device: root moves of all "
+                                 "positions share the divide tags, every level and the final stage one grid); "
+                                 "final_kernel_ms is that one final stage",
+                         "streams": "one context (stream) per position, every position's repeat runs enqueued "
+                                    "before any wait"}[how] +
+                        "; positions[].ms_per_step and sequential_ms_per_step time the positions one after another")
         out["sequential_ms_per_step"] = seq_ms
     rec = _pmc(pmc_key) if d.world == 1 else None
     if rec and kl and kms > 0:

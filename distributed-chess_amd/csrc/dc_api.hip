@@ -149,13 +149,14 @@ struct dc_ctx {
   // The last perft launch sequence, captured as a hipGraph (see perft_run).
   struct PerftKey {
     u32 rules, depth, split, shard, n_shards, stm, k4;
+    u32 n_root;  // root positions expanded together (dc_perft_batch; 1 otherwise)
     uint64_t epoch;
     // the capacities a captured graph was sized with (test knobs
     // DCHESS_PERFT_WIDE_MAX / _WIDE_LEVEL_MAX): a changed knob re-captures
     uint64_t wide_words, wide_level;
     bool operator==(const PerftKey& o) const {
       return rules == o.rules && depth == o.depth && split == o.split && shard == o.shard &&
-             n_shards == o.n_shards && stm == o.stm && k4 == o.k4 && epoch == o.epoch &&
+             n_shards == o.n_shards && stm == o.stm && k4 == o.k4 && n_root == o.n_root && epoch == o.epoch &&
              wide_words == o.wide_words && wide_level == o.wide_level;
     }
   } pkey{};
@@ -173,8 +174,9 @@ struct dc_ctx {
   bool last_exact = false;
   const char* last_final = "count2";  // timing name of the last perft's final stage
   struct RootStage {
-    Board b;
-    uint16_t meta;
+    Board b[dc::kMaxPerftRoots];
+    uint16_t meta[dc::kMaxPerftRoots];
+    u32 n;
   }* root_host = nullptr;  // pinned
   // batch / replay scratch
   DBuf<DevPos> pos;
@@ -1322,16 +1324,35 @@ static bool shard_contiguous() {
 // the block when it executes) must see the value they were queued with, so a
 // changed root first waits for the stream.  A capture only ever re-stages the
 // root of the run that was just synchronised (the value is unchanged).
-int write_root_host(dc_ctx* c, const dc_pos* pos) {
-  const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
-  const uint16_t rm = dc::pack_meta(pos->castle, pos->ep);
-  if (std::memcmp(&c->root_host->b, &rb, sizeof(Board)) == 0 && c->root_host->meta == rm) return DC_SUCCESS;
+bool root_staged(const dc_ctx* c, const dc_pos* pos, u32 n) {
+  if (c->root_host->n != n) return false;
+  for (u32 i = 0; i < n; ++i) {
+    const Board rb{pos[i].bb[0], pos[i].bb[1], pos[i].bb[2], pos[i].bb[3]};
+    if (std::memcmp(&c->root_host->b[i], &rb, sizeof(Board)) != 0 ||
+        c->root_host->meta[i] != dc::pack_meta(pos[i].castle, pos[i].ep))
+      return false;
+  }
+  return true;
+}
+
+int write_root_host(dc_ctx* c, const dc_pos* pos, u32 n = 1) {
+  if (root_staged(c, pos, n)) return DC_SUCCESS;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   HIP_TRY(hipStreamIsCapturing(c->stream, &cs));
   if (cs != hipStreamCaptureStatusNone) return DC_EHIP;  // unreachable: captures follow a synchronised run
   HIP_TRY(hipStreamSynchronize(c->stream));
-  c->root_host->b = rb;
-  c->root_host->meta = rm;
+  for (u32 i = 0; i < n; ++i) {
+    c->root_host->b[i] = Board{pos[i].bb[0], pos[i].bb[1], pos[i].bb[2], pos[i].bb[3]};
+    c->root_host->meta[i] = dc::pack_meta(pos[i].castle, pos[i].ep);
+  }
+  c->root_host->n = n;
+  return DC_SUCCESS;
+}
+
+// the staged roots to the device root arrays (stream-ordered)
+int upload_roots(dc_ctx* c, u32 n) {
+  HIP_TRY(hipMemcpyAsync(c->root.p, c->root_host->b, n * sizeof(Board), hipMemcpyHostToDevice, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->root_meta.p, c->root_host->meta, n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   return DC_SUCCESS;
 }
 
@@ -1359,7 +1380,8 @@ static bool fide_top_short() {
 // (exact mode or a level beyond the speculative budget): such a sequence
 // depends on data and is never captured as a graph.
 int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
-                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true) {
+                  uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true,
+                  u32 n_pos = 1) {
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
@@ -1392,11 +1414,14 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   static const u64 kTopCap[4] = {1, 256, 256 * 256, 1ull << 20};
   // buffers (allocated before anything is enqueued)
   if (!c->res_host) HIP_TRY(hipHostMalloc((void**)&c->res_host, sizeof(dc::PerftResult)));
-  if (!c->root_host) HIP_TRY(hipHostMalloc((void**)&c->root_host, sizeof(*c->root_host)));
+  if (!c->root_host) {
+    HIP_TRY(hipHostMalloc((void**)&c->root_host, sizeof(*c->root_host)));
+    c->root_host->n = 0;
+  }
   HIP_TRY(c->res.ensure(1));
   HIP_TRY(c->rng.ensure(16));
-  HIP_TRY(c->root.ensure(1));
-  HIP_TRY(c->root_meta.ensure(1));
+  HIP_TRY(c->root.ensure(dc::kMaxPerftRoots));
+  HIP_TRY(c->root_meta.ensure(dc::kMaxPerftRoots));
   HIP_TRY(c->top_nodes.ensure(kTopCap[1] + kTopCap[2]));
   HIP_TRY(c->top_tags.ensure(kTopCap[1] + kTopCap[2]));
   if (fide) HIP_TRY(c->top_meta.ensure(kTopCap[1] + kTopCap[2]));
@@ -1413,10 +1438,9 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   }
   // root upload from pinned memory (stage_root = false: the caller staged it)
   if (stage_root) {
-    e = write_root_host(c, pos);
+    e = write_root_host(c, pos, n_pos);
+    if (e == DC_SUCCESS) e = upload_roots(c, n_pos);
     if (e != DC_SUCCESS) return e;
-    HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
   // REF final stage over the last three plies (k_count3c): the level F is
   // never written; its parents' level is counted and scanned, then expanded
@@ -1447,7 +1471,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   HIP_TRY(c->timed("expand_top", 0, [&] {
     return dc::launch_expand_top(c->stream, rules, c->root.p, c->root_meta.p, pos->stm, T, ts, c->nodes[0].p,
                                  fide ? c->meta[0].p : nullptr, c->tags[0].p, cap_T, c->res.p, c->rng.p + T,
-                                 top_words ? c->top_words.p : nullptr);
+                                 top_words ? c->top_words.p : nullptr, n_pos);
   }));
   u32 L = T;
   u64 nb = cap_T;
@@ -1658,12 +1682,12 @@ static bool perft_graphs_enabled() {
 // which removes the per-kernel launch gaps.  The root position
 // is read from the pinned staging block when the graph runs.
 int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
-              uint32_t n_shards, bool exact, dc::PerftResult* out) {
+              uint32_t n_shards, bool exact, dc::PerftResult* out, u32 n_pos = 1) {
   const bool graphable = !exact && !c->profiling && perft_graphs_enabled();
-  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
+  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(), n_pos,
                        g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
   if (graphable && c->pgraph && c->pkey == key) {
-    int e = write_root_host(c, pos);
+    int e = write_root_host(c, pos, n_pos);
     if (e != DC_SUCCESS) return e;
     HIP_TRY(hipGraphLaunch(c->pgraph, c->stream));
     e = sync_ctx(c);
@@ -1672,7 +1696,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
     return DC_SUCCESS;
   }
   bool host_sync = false;
-  int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, exact, &host_sync);
+  int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, exact, &host_sync, true, n_pos);
   if (e != DC_SUCCESS) return e;
   HIP_TRY(hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream));
   e = sync_ctx(c);
@@ -1690,7 +1714,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
     return DC_SUCCESS;
   }
   bool hs = false;
-  int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs);
+  int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, true, n_pos);
   if (ce == DC_SUCCESS &&
       hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
     ce = DC_EHIP;
@@ -1708,7 +1732,8 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
 }
 
 int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
-               uint32_t n_shards, uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total) {
+               uint32_t n_shards, uint64_t* divide, uint16_t* root_moves, uint32_t* n_root, uint64_t* total,
+               u32 n_pos = 1, uint8_t* root_parent = nullptr) {
   if (!pos || !total || rules > DC_RULES_FIDE || n_shards == 0 || shard >= n_shards || pos->stm > 1) return DC_EINVAL;
   if (depth > 12) return DC_EUNSUPPORTED;
   *total = 0;
@@ -1718,14 +1743,15 @@ int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uin
     return DC_SUCCESS;
   }
   dc::PerftResult r;
-  int e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r);
+  int e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r, n_pos);
   c->last_exact = e == DC_SUCCESS && r.overflow;
-  if (c->last_exact) e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, true, &r);
+  if (c->last_exact) e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, true, &r, n_pos);
   if (e != DC_SUCCESS) return e;
   if (r.overflow) return DC_EUNSUPPORTED;  // more than 256 root moves, or a level beyond 2^32 nodes
   const u32 nr = r.n_root;
   if (n_root) *n_root = nr;
   if (root_moves) std::copy(r.root_moves, r.root_moves + nr, root_moves);
+  if (root_parent) std::copy(r.root_parent, r.root_parent + nr, root_parent);
   u64 t = 0;
   for (u32 i = 0; i < nr; ++i) {
     const u64 v = depth == 1 ? (shard == 0 ? 1 : 0) : r.divide[i];
@@ -1766,10 +1792,11 @@ int dc_perft_shard(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth,
 constexpr u32 kRepeatBatch = 8;
 
 static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
-                       uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out, u32 idx0, u32 stride) {
+                       uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out, u32 idx0, u32 stride,
+                       u32 n_pos = 1) {
   if (n_runs == 0) return DC_SUCCESS;
   HIP_TRY(c->rcur.ensure(1));  // before the key: an allocation moves the epoch
-  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(),
+  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(), n_pos,
                        g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
   const bool graphable = !c->profiling && perft_graphs_enabled();
   // capture `runs` runs of the sequence back to back (the result copy is part
@@ -1779,7 +1806,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
     bool hs = false;
     int ce = DC_SUCCESS;
     for (u32 r = 0; r < runs && ce == DC_SUCCESS && !hs; ++r) {
-      ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false);
+      ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false, n_pos);
       if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
     }
     hipGraph_t g = nullptr;
@@ -1795,7 +1822,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
     // a plain run (host sync) sizes the buffers and stages the root; then the
     // sequence is captured without the root upload and the readback
     uint64_t total = 0;
-    int e = perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, nullptr, nullptr, nullptr, &total);
+    int e = perft_impl(c, rules, pos, depth, split_depth, shard, n_shards, nullptr, nullptr, nullptr, &total, n_pos);
     if (e != DC_SUCCESS) return e;
     if (c->last_exact) {
       // speculative capacities overflow for this configuration: exact runs
@@ -1803,7 +1830,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
       HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out), idx0, stride));
       for (u32 i = 0; i < n_runs; ++i) {
         bool hs = false;
-        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs);
+        e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, true, &hs, true, n_pos);
         if (e != DC_SUCCESS) return e;
         HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
       }
@@ -1826,16 +1853,13 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
     }
   }
   const bool use_graph = graphable && c->rgraph && c->rkey == key;
-  const Board rb{pos->bb[0], pos->bb[1], pos->bb[2], pos->bb[3]};
-  const uint16_t rm = dc::pack_meta(pos->castle, pos->ep);
-  if (use_graph && (std::memcmp(&c->root_host->b, &rb, sizeof(Board)) != 0 || c->root_host->meta != rm)) {
+  if (use_graph && !root_staged(c, pos, n_pos)) {
     // every staging copies root_host to the device root, so the device root
     // holds *pos once queued work is done if root_host does; else restage
     // (write_root_host waits for the runs still queued to read the pinned block)
-    int e = write_root_host(c, pos);
+    int e = write_root_host(c, pos, n_pos);
+    if (e == DC_SUCCESS) e = upload_roots(c, n_pos);
     if (e != DC_SUCCESS) return e;
-    HIP_TRY(hipMemcpyAsync(c->root.p, &c->root_host->b, sizeof(Board), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->root_meta.p, &c->root_host->meta, sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
   }
   HIP_TRY(dc::launch_set_result_cursor(c->stream, c->rcur.p, reinterpret_cast<u64*>(d_out), idx0, stride));
   u32 i = 0;
@@ -1851,7 +1875,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
       HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
     } else {
       bool host_sync = false;
-      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync);
+      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync, true, n_pos);
       if (e != DC_SUCCESS) return e;
       HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
     }
@@ -1870,6 +1894,49 @@ int dc_perft_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_
   // run's front end would overlap the other's final stage: 1.03 against
   // 0.53 ms per perft(7) step; not kept)
   return repeat_runs(c, rules, pos, depth, split_depth, shard, n_shards, n_runs, d_out, 0, 1);
+}
+
+// A batch of root positions with the same side to move as one tree: the top
+// kernel expands them together, their root moves (at most 256 in all) share
+// the divide tags, and every level after it -- the final stage included --
+// holds all of them, so the GPU runs one full grid per level instead of one
+// small one per position (BASELINE configs[2]: six suite positions at depth 5).
+static_assert(DC_PERFT_BATCH_MAX == dc::kMaxPerftRoots, "dchess.h batch bound");
+static int batch_args(uint32_t rules, const dc_pos* pos, uint32_t n_pos, uint32_t depth) {
+  if (!pos || n_pos == 0 || rules > DC_RULES_FIDE) return DC_EINVAL;
+  if (n_pos > dc::kMaxPerftRoots || depth == 0 || depth > 12) return DC_EUNSUPPORTED;
+  for (u32 i = 0; i < n_pos; ++i)
+    if (pos[i].stm > 1 || pos[i].stm != pos[0].stm) return DC_EINVAL;
+  return DC_SUCCESS;
+}
+
+int dc_perft_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t n_pos, uint32_t depth, uint64_t* totals,
+                   uint64_t* divide, uint16_t* root_moves, uint8_t* root_pos, uint32_t* n_root) {
+  ENTER_WORK(c);
+  int e = batch_args(rules, pos, n_pos, depth);
+  if (e != DC_SUCCESS) return e;
+  if (!totals) return DC_EINVAL;
+  uint64_t div[256], total = 0;
+  uint8_t parent[256];
+  uint32_t nr = 0;
+  e = perft_impl(c, rules, pos, depth, 1, 0, 1, div, root_moves, &nr, &total, n_pos, parent);
+  if (e != DC_SUCCESS) return e;
+  for (u32 i = 0; i < n_pos; ++i) totals[i] = 0;
+  for (u32 k = 0; k < nr; ++k) totals[parent[k] < n_pos ? parent[k] : 0] += div[k];
+  if (divide) std::copy(div, div + nr, divide);
+  if (root_pos) std::copy(parent, parent + nr, root_pos);
+  if (n_root) *n_root = nr;
+  return DC_SUCCESS;
+}
+
+int dc_perft_batch_repeat_device(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t n_pos, uint32_t depth,
+                                 uint32_t split_depth, uint32_t n_runs, uint64_t* d_out) {
+  ENTER_WORK(c);
+  int e = batch_args(rules, pos, n_pos, depth);
+  if (e != DC_SUCCESS) return e;
+  if (n_runs && !d_out) return DC_EINVAL;
+  if (depth < 2) return DC_EUNSUPPORTED;
+  return repeat_runs(c, rules, pos, depth, split_depth, 0, 1, n_runs, d_out, 0, 1, n_pos);
 }
 
 int dc_ctx_synchronize(dc_ctx* c) {

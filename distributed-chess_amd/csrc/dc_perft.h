@@ -20,7 +20,12 @@ struct PerftResult {
   u64 level_n[16];
   u32 dfs_next;    // k_perft_dfs's frontier cursor (zeroed with the block)
   u32 pad0;
+  uint8_t root_parent[256];  // which root position each root move belongs to (a batch: dc_perft_batch)
 };
+
+// Root positions one launch sequence can expand together (dc_perft_batch): the
+// top kernel stages them in LDS; their root moves share the 256 divide tags.
+constexpr u32 kMaxPerftRoots = 8;
 
 // Scratch of the single-workgroup top expansion (plies 1 and 2).
 struct TopScratch {
@@ -32,7 +37,7 @@ struct TopScratch {
 
 hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const uint16_t* root_meta, u32 stm0,
                              u32 target, const TopScratch& s, Board* out, uint16_t* out_meta, uint16_t* out_tags,
-                             u64 cap_out, PerftResult* res, Range* out_rng, u32* words = nullptr);
+                             u64 cap_out, PerftResult* res, Range* out_rng, u32* words = nullptr, u32 n_root = 1);
 // words != nullptr (target ply >= 2): k_expand_top leaves the target ply as
 // move words {parent << 15 | f | t << 6 | promo << 12} over the previous top
 // ply (s.nodes[target - 2]); launch_make_count then makes, stores and counts

@@ -357,7 +357,10 @@ __device__ __forceinline__ void top_level(const Board* cur, const uint16_t* cur_
       if constexpr (R::kMeta) nxt_meta[oo] = (uint16_t)cm;
       if (root) {
         nxt_tags[oo] = (uint16_t)oo;
-        if (oo < 256) res->root_moves[oo] = (uint16_t)(f | (to << 6) | (promo << 12));
+        if (oo < 256) {
+          res->root_moves[oo] = (uint16_t)(f | (to << 6) | (promo << 12));
+          res->root_parent[oo] = (uint8_t)pl;
+        }
       } else {
         nxt_tags[oo] = stage ? stags[pl] : cur_tags[pl];
       }
@@ -381,7 +384,7 @@ __global__ __launch_bounds__(R::kTopThreads) void k_expand_top(const Board* __re
                                                              uint16_t* __restrict__ out_meta,
                                                              uint16_t* __restrict__ out_tags, u64 cap_out,
                                                              PerftResult* __restrict__ res, Range* __restrict__ out_rng,
-                                                             u32* __restrict__ words) {
+                                                             u32* __restrict__ words, u32 n_root) {
   constexpr int kTopThreads = R::kTopThreads;  // (shadows the file-wide 1024)
   __shared__ u64 wsum[kTopThreads / 64];
   __shared__ u64 s_total;
@@ -392,22 +395,23 @@ __global__ __launch_bounds__(R::kTopThreads) void k_expand_top(const Board* __re
   __shared__ uint16_t smeta[R::kMeta ? kTopStage : 1];
   __shared__ uint16_t stags[kTopStage];
   __shared__ uint16_t s_root_tag;
-  __shared__ Board s_root;
-  __shared__ uint16_t s_root_meta;
+  __shared__ Board s_root[kMaxPerftRoots];  // one position, or a batch's (dc_perft_batch)
+  __shared__ uint16_t s_root_meta[kMaxPerftRoots];
   // the run's result block is cleared here, not by a separate memset launch
   // (one ~5 us graph node less per perft)
   static_assert(sizeof(PerftResult) % 8 == 0, "PerftResult is cleared in u64 words");
   for (u32 k = threadIdx.x; k < sizeof(PerftResult) / 8; k += kTopThreads) reinterpret_cast<u64*>(res)[k] = 0;
-  if (threadIdx.x == 0) {
-    s_root_tag = 0;
-    s_root = root[0];
-    s_root_meta = R::kMeta ? root_meta[0] : (uint16_t)0;
+  n_root = min(max(n_root, 1u), kMaxPerftRoots);  // (the host checks the count)
+  if (threadIdx.x == 0) s_root_tag = 0;
+  if (threadIdx.x < n_root) {
+    s_root[threadIdx.x] = root[threadIdx.x];
+    s_root_meta[threadIdx.x] = R::kMeta ? root_meta[threadIdx.x] : (uint16_t)0;
   }
   __syncthreads();
-  const Board* cur = &s_root;
-  const uint16_t* cur_meta = &s_root_meta;
-  const uint16_t* cur_tags = &s_root_tag;
-  u64 n = 1;
+  const Board* cur = s_root;
+  const uint16_t* cur_meta = s_root_meta;
+  const uint16_t* cur_tags = &s_root_tag;  // (ply 1 tags each child by its index: roots need none)
+  u64 n = n_root;
   for (u32 ply = 1; ply <= target; ++ply) {
     const bool last = ply == target;
     Board* dst = last ? out : sb.nodes[ply - 1];
@@ -1923,7 +1927,7 @@ static u32 resident_grid(K kernel, u32 block, u32 want) {
 
 hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const uint16_t* root_meta, u32 stm0,
                              u32 target, const TopScratch& s, Board* out, uint16_t* out_meta, uint16_t* out_tags,
-                             u64 cap_out, PerftResult* res, Range* out_rng, u32* words) {
+                             u64 cap_out, PerftResult* res, Range* out_rng, u32* words, u32 n_root) {
   TopBufs b;
   for (int k = 0; k < 2; ++k) {
     b.nodes[k] = s.nodes[k];
@@ -1933,10 +1937,10 @@ hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const
   }
   if (rules == 0)
     hipLaunchKernelGGL(k_expand_top<RefRules>, dim3(1), dim3(RefRules::kTopThreads), 0, st, root, root_meta, stm0, target, b, out,
-                       out_meta, out_tags, cap_out, res, out_rng, words);
+                       out_meta, out_tags, cap_out, res, out_rng, words, n_root);
   else
     hipLaunchKernelGGL(k_expand_top<FideRules>, dim3(1), dim3(FideRules::kTopThreads), 0, st, root, root_meta, stm0, target, b,
-                       out, out_meta, out_tags, cap_out, res, out_rng, words);
+                       out, out_meta, out_tags, cap_out, res, out_rng, words, n_root);
   return hipGetLastError();
 }
 

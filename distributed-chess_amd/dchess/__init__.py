@@ -100,6 +100,10 @@ def lib():
                                      _vp, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
         "dc_perft_repeat_device": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                              C.c_uint32, _vp]),
+        "dc_perft_batch": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.c_uint32, _vp, _vp, _vp, _vp,
+                                     C.POINTER(C.c_uint32)]),
+        "dc_perft_batch_repeat_device": (C.c_int, [_vp, C.c_uint32, _vp, C.c_uint32, C.c_uint32, C.c_uint32,
+                                                   C.c_uint32, _vp]),
         "dc_ctx_synchronize": (C.c_int, [_vp]),
         "dc_multi_perft": (C.c_int, [_vp, C.c_int, C.c_uint32, _vp, C.c_uint32, _vp, _vp, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint64)]),
@@ -504,6 +508,29 @@ class Engine:
         ptr = d_out.ptr if hasattr(d_out, "ptr") else _vp(int(d_out))
         _check(lib().dc_perft_repeat_device(self.ctx, rules, _ptr(p), depth, split_depth, shard, n_shards, n_runs,
                                             ptr), "dc_perft_repeat_device")
+
+    def perft_batch(self, positions, depth, rules=RULES_REF):
+        """dc_perft_batch: the positions (same side to move) counted as one tree.
+        Returns (totals[n_pos], divide[n_root], root_moves[n_root], root_pos[n_root])."""
+        p = np.array(list(positions), POS_DTYPE)
+        tot = np.zeros(len(p), np.uint64)
+        div = np.zeros(256, np.uint64)
+        rm = np.zeros(256, np.uint16)
+        rp = np.zeros(256, np.uint8)
+        nr = C.c_uint32()
+        _check(lib().dc_perft_batch(self.ctx, rules, _ptr(p), len(p), depth, _ptr(tot), _ptr(div), _ptr(rm), _ptr(rp),
+                                    C.byref(nr)), "dc_perft_batch")
+        n = nr.value
+        return tot, div[:n].copy(), rm[:n].copy(), rp[:n].copy()
+
+    def perft_batch_repeat_device(self, positions, depth, split_depth, n_runs, d_out, rules=RULES_REF):
+        """dc_perft_batch_repeat_device: n_runs batch perfts enqueued back to back,
+        records as perft_repeat_device (per-position totals: sum divide over
+        perft_batch's root_pos)."""
+        p = np.array(list(positions), POS_DTYPE)
+        ptr = d_out.ptr if hasattr(d_out, "ptr") else _vp(int(d_out))
+        _check(lib().dc_perft_batch_repeat_device(self.ctx, rules, _ptr(p), len(p), depth, split_depth, n_runs, ptr),
+               "dc_perft_batch_repeat_device")
 
     def synchronize(self):
         _check(lib().dc_ctx_synchronize(self.ctx), "dc_ctx_synchronize")

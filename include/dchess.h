@@ -322,6 +322,24 @@ int dc_perft_shard(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t dept
  * each run's divide vector). */
 int dc_perft_repeat_device(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
                            uint32_t shard, uint32_t n_shards, uint32_t n_runs, uint64_t* d_out);
+
+/* perft of a batch of n_pos (1..DC_PERFT_BATCH_MAX) positions with the same side
+ * to move, counted as one tree: their root moves (at most 256 in all; more is
+ * DC_EUNSUPPORTED) share the divide tags, so every level -- the final stage's
+ * included -- holds all positions and runs one grid instead of one per position
+ * (a perft suite: BASELINE configs[2], the six published positions at depth 5).
+ * totals[i] = perft(pos[i], depth); divide / root_moves as dc_perft over the
+ * concatenated root moves, root_pos[k] = the position root move k belongs to
+ * (each may be NULL; room for 256 entries). */
+#define DC_PERFT_BATCH_MAX 8
+int dc_perft_batch(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t n_pos, uint32_t depth, uint64_t* totals,
+                   uint64_t* divide, uint16_t* root_moves, uint8_t* root_pos, uint32_t* n_root);
+/* n_runs batch perfts enqueued as dc_perft_repeat_device does (depth >= 2, one
+ * shard): run i's 258-word record in DEVICE memory holds the concatenated
+ * divide ([257] = the batch's total); per-position totals are the sums of the
+ * divide entries over dc_perft_batch's root_pos. */
+int dc_perft_batch_repeat_device(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t n_pos, uint32_t depth,
+                                 uint32_t split_depth, uint32_t n_runs, uint64_t* d_out);
 /* Blocks until all work queued on the context stream has finished. */
 int dc_ctx_synchronize(dc_ctx* ctx);
 

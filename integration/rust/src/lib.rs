@@ -142,6 +142,11 @@ pub mod sys {
         pub fn dc_perft_repeat_device(ctx: *mut dc_ctx, rules: u32, pos: *const dc_pos, depth: u32,
                                       split_depth: u32, shard: u32, n_shards: u32, n_runs: u32,
                                       d_out: *mut u64) -> c_int;
+        pub fn dc_perft_batch(ctx: *mut dc_ctx, rules: u32, pos: *const dc_pos, n_pos: u32, depth: u32,
+                              totals: *mut u64, divide: *mut u64, root_moves: *mut u16, root_pos: *mut u8,
+                              n_root: *mut u32) -> c_int;
+        pub fn dc_perft_batch_repeat_device(ctx: *mut dc_ctx, rules: u32, pos: *const dc_pos, n_pos: u32,
+                                            depth: u32, split_depth: u32, n_runs: u32, d_out: *mut u64) -> c_int;
         pub fn dc_ctx_synchronize(ctx: *mut dc_ctx) -> c_int;
         // multi-GPU
         pub fn dc_multi_perft(devices: *const c_int, n_devices: c_int, rules: u32, pos: *const dc_pos, depth: u32,
