@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--hash-steps", type=int, default=3)
     ap.add_argument("--txs", type=int, default=262_144, help="signature leg: transactions per rank (0: off)")
     ap.add_argument("--tx-steps", type=int, default=3)
+    ap.add_argument("--suite-batch-only", action="store_true",
+                    help="FIDE suite leg: the batch alone, no per-position runs (its PMC pass: one kind of dispatch)")
     ap.add_argument("--only", default="", help="comma-separated legs to run (rocprof passes): " + ", ".join(LEGS))
     return ap.parse_args()
 
@@ -776,7 +778,8 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
     steps = max(2, args.steps // 4)
     leaves, dt, per = 0, 0.0, {}
     kms, kunits, kl = 0.0, 0, 0
-    for k in keys:
+    batched = len(keys) > 1 and d.dist is None
+    for k in ([] if batched and args.suite_batch_only else keys):
         pos = dchess.pos_from_fen(_OG[k]["fen"])
         want = _OG[k]["perft"][str(depth)]
         lv, t = timed_perft(eng, d, args, pos, depth, steps, 1, rules=dchess.RULES_FIDE, want=want)
@@ -794,7 +797,8 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
         kl += ks["launches"]
         kunits += want // d.world
     seq_ms = 1e3 * dt / steps
-    batched = len(keys) > 1 and d.dist is None
+    if batched and args.suite_batch_only:
+        kunits = sum(_OG[k]["perft"][str(depth)] for k in keys) // d.world
     how = None
     if batched:  # the suite as one batch: the leg's value
         items = [(dchess.pos_from_fen(_OG[k]["fen"]), _OG[k]["perft"][str(depth)]) for k in keys]

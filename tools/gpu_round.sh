@@ -58,6 +58,7 @@ if has fidepmc; then
   rm -rf $O/pmc_f*
   for leg in fide7 fidesuite; do
     P="--steps 4 --warmup 1 --no-cpu --only $leg"
+    [ $leg = fidesuite ] && P="$P --suite-batch-only"  # one kind of k_count2b dispatch: the six-position batch
     fpass() { local c=$1 t=$2; step "pmc $t"; timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/pmc_$t -o p -- python bench.py $P > /dev/null 2>> $O/pmc.err; }
     fpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" f1$leg && \
     fpass "FETCH_SIZE" f2$leg && fpass "WRITE_SIZE" f3$leg && \
@@ -67,8 +68,8 @@ if has fidepmc; then
   done
   python tools/pmc_summary.py $O/fide7 --json $O/pmc_fide7.json --source "rocprofv3 --pmc (4 passes), bench.py --only fide7" \
     --units "fide_d7=k_count2b<dc::FideRules=3195901860" > $O/pmc_fide.txt
-  python tools/pmc_summary.py $O/fidesuite --json $O/pmc_fidesuite.json --source "rocprofv3 --pmc (4 passes), bench.py --only fidesuite" \
-    --units "fide_suite_d5=k_count2b<dc::FideRules=78180160" >> $O/pmc_fide.txt
+  python tools/pmc_summary.py $O/fidesuite --json $O/pmc_fidesuite.json --source "rocprofv3 --pmc (4 passes), bench.py --only fidesuite --suite-batch-only" \
+    --units "fide_suite_d5=k_count2b<dc::FideRules=469080960" >> $O/pmc_fide.txt
   python - <<'PY'
 import json, os
 p = "gpurun_out/pmc_latest.json"
