@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--hash-steps", type=int, default=3)
     ap.add_argument("--txs", type=int, default=262_144, help="signature leg: transactions per rank (0: off)")
     ap.add_argument("--tx-steps", type=int, default=3)
+    ap.add_argument("--perft-streams", type=int, default=0,
+                    help="contexts a repeated perft's steps are split over (0: 3 at depth <= 6, 2 at 7, 1 deeper)")
     ap.add_argument("--suite-batch-only", action="store_true",
                     help="FIDE suite leg: the batch alone, no per-position runs (its PMC pass: one kind of dispatch)")
     ap.add_argument("--only", default="", help="comma-separated legs to run (rocprof passes): " + ", ".join(LEGS))
@@ -213,6 +215,46 @@ def cpu_baselines(args, threads, replay_host=None):
 REPEAT_BATCH = 8  # runs per batch graph of dc_perft_repeat_device (dc_api.hip kRepeatBatch)
 
 
+_ENGINES = {}
+
+
+def perft_contexts(eng, d, n):
+    """`eng` plus n - 1 more contexts (streams) on this rank's GPU, kept for the
+    whole bench (their level buffers and captured graphs are reused)."""
+    extra = _ENGINES.setdefault(d.device, [])
+    while len(extra) < n - 1:
+        extra.append(dchess.Engine(d.device))
+    return [eng] + extra[:n - 1]
+
+
+def perft_streams(args, depth):
+    """Contexts a repeated perft(depth) is spread over.  One perft's front end
+    (the one-workgroup top expansion and the level chain before the final stage,
+    ~70 us) is latency-bound; with the steps split over two or three contexts --
+    streams -- one run's front end executes while another's final stage holds
+    the CUs (tools/overlap_perft.py, profiles/r05/overlap_u.jsonl: perft(7)
+    0.408 -> 0.378 ms per step with 2, perft(6) 0.068 -> 0.034 with 3).  Every
+    step is still a whole perft with its own result record.  Deep runs (the
+    final stage is everything) keep one."""
+    if args.perft_streams:
+        return args.perft_streams
+    return 3 if depth <= 6 else 2 if depth == 7 else 1
+
+
+def enqueue_split(engs, steps, base_ptr, W, fn):
+    """fn(engine, n_runs, device_address) for each context's share of `steps`
+    runs, its records at consecutive slots of the one result array."""
+    n = len(engs)
+    k0 = 0
+    for i, e in enumerate(engs):
+        k = steps // n + (1 if i < steps % n else 0)
+        if k:
+            fn(e, k, base_ptr + k0 * W * 8)
+        k0 += k
+    for e in engs:
+        e.synchronize()
+
+
 def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF, want=None):
     """warmup + exactly `steps` timed perft(depth) steps (barrier + device sync on
     both sides, max over ranks), parity-checked against the golden count.
@@ -234,17 +276,25 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF,
     # the first dc_perft_repeat_device call of a configuration runs one plain
     # perft and captures the launch graphs (one run, and a batch of
     # REPEAT_BATCH runs): do it here, outside the timed region
-    nw = REPEAT_BATCH if steps >= REPEAT_BATCH else 1  # (fewer steps never launch the batch graph)
-    warm = eng.alloc(nw * W * 8)
-    eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, nw, warm, rules=rules)
-    eng.synchronize()
+    engs = perft_contexts(eng, d, max(1, min(perft_streams(args, depth), steps)))
+    share = -(-steps // len(engs))
+    warm = eng.alloc(REPEAT_BATCH * W * 8)
+    for e in engs:  # every context captures its graphs (one run; a batch of REPEAT_BATCH when its share has one)
+        for nw in ((1, REPEAT_BATCH) if share >= REPEAT_BATCH else (1,)):
+            e.perft_repeat_device(pos, depth, args.split, d.rank, d.world, nw, warm, rules=rules)
+        e.synchronize()
     warm.free()
+
+    def run(e, k, ptr):
+        e.perft_repeat_device(pos, depth, args.split, d.rank, d.world, k, ptr, rules=rules)
+
     if d.dist is None:
         buf = eng.alloc(steps * W * 8)
+        if len(engs) > 1:  # one untimed pass of the split (the first concurrent graph launches run slower)
+            enqueue_split(engs, steps, buf.ptr.value, W, run)
         d.sync()
         t0 = time.perf_counter()
-        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, buf, rules=rules)
-        eng.synchronize()
+        enqueue_split(engs, steps, buf.ptr.value, W, run)
         d.sync()
         dt = time.perf_counter() - t0
         res = buf.download(np.uint64, steps * W).reshape(steps, W)
@@ -253,10 +303,12 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF,
     else:
         torch = d.torch
         t = torch.zeros((steps, W), dtype=torch.int64, device=f"cuda:{d.device}")
+        if len(engs) > 1:  # one untimed pass of the split, as above
+            enqueue_split(engs, steps, t.data_ptr(), W, run)
+            t.zero_()
         d.sync()
         t0 = time.perf_counter()
-        eng.perft_repeat_device(pos, depth, args.split, d.rank, d.world, steps, t.data_ptr(), rules=rules)
-        eng.synchronize()
+        enqueue_split(engs, steps, t.data_ptr(), W, run)
         # the exchange step of every timed perft, bucketed: one RCCL all-reduce
         # (over xGMI) of all steps' per-root-move vectors, n_root words and totals
         if d.cdev == "cpu":  # gloo rehearsal: the collective on a host copy
@@ -742,14 +794,18 @@ def batch_perfts(eng, d, args, items, depth, steps, rules):
     if [int(x) for x in tot] != want:
         raise SystemExit(f"parity failure: batch FIDE perft({depth}) = {list(tot)}, expected {want}")
     b = eng.alloc(max(REPEAT_BATCH, steps) * W * 8)
-    for nw in (1, REPEAT_BATCH):  # graph captures (the one-run and the batch graph)
-        eng.perft_batch_repeat_device(pos, depth, args.split, nw, b, rules=rules)
-    eng.perft_batch_repeat_device(pos, depth, args.split, steps, b, rules=rules)  # one untimed pass
-    eng.synchronize()
+    engs = perft_contexts(eng, d, max(1, min(args.perft_streams or 2, steps)))  # (front end ~80 us of ~0.46 ms)
+
+    def run(e, k, ptr):
+        e.perft_batch_repeat_device(pos, depth, args.split, k, ptr, rules=rules)
+
+    for e in engs:
+        for nw in (1, REPEAT_BATCH):  # graph captures (the one-run and the batch graph)
+            run(e, nw, b.ptr.value)
+    enqueue_split(engs, steps, b.ptr.value, W, run)  # one untimed pass
     d.sync()
     t0 = time.perf_counter()
-    eng.perft_batch_repeat_device(pos, depth, args.split, steps, b, rules=rules)
-    eng.synchronize()
+    enqueue_split(engs, steps, b.ptr.value, W, run)
     d.sync()
     dt = time.perf_counter() - t0
     res = b.download(np.uint64, steps * W).reshape(steps, W)
@@ -966,7 +1022,7 @@ def main():
         l6, dt6 = timed_perft(eng, d, args, pos, 6, 4 * args.steps, args.warmup)
         p6 = {"value": l6 / dt6, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt6 / (4 * args.steps),
               "steps": 4 * args.steps, "workload": "perft(startpos, 6) RULES_REF, frontier split at ply 3",
-              "scaling": "strong"}
+              "scaling": "strong", "streams_per_gpu": perft_streams(args, 6)}
     if "perft8" in legs:
         note("perft8")
         p8 = perft8_leg(eng, d, args, pos)
@@ -1014,7 +1070,12 @@ def main():
                                f"frontier split at ply {args.split} into strided shards over ranks, "
                                "per-root-move counts all-reduced over RCCL",
                    "depth": args.depth, "rules": "REF", "leaves_per_step": REF_STARTPOS.get(args.depth),
-                   "parallelism": f"dp{d.world}"},
+                   "parallelism": f"dp{d.world}",
+                   "streams_per_gpu": perft_streams(args, args.depth),
+                   "streams_note": "the K timed steps are split over this many contexts (HIP streams) per GPU, "
+                                   "each enqueuing its share at once; each step is a whole perft with its own "
+                                   "result record, and one run's latency-bound front end overlaps another's "
+                                   "final stage"},
     }
     if ks is not None:
         line["roofline"] = roofline(ks, args.depth, d.world)
