@@ -449,6 +449,42 @@ def test_perft_repeat_device_batches(engine):
         assert (res[:, 257] == want).all(), res[:, 257]
 
 
+def test_perft_repeat_device_split_over_contexts(engine):
+    """The bench's timed perft steps split over concurrent contexts (bench.py
+    enqueue_split): three contexts -- three streams -- enqueue their shares of
+    whole runs at once, each into its slots of ONE result array allocated by
+    another context, two of them with a different position; every record is
+    the right whole perft."""
+    W = 258
+    s = dchess.startpos()
+    mid = dchess.pos_from_fen("rnbqkbnr/pppp1ppp/8/4p3/4P3/8/PPPP1PPP/RNBQKBNR w - - 0 2")
+    want_mid, _, _ = engine.perft(mid, 6)
+    want_s = 120909581  # REF perft(6) of startpos (tests/golden)
+    others = [dchess.Engine(0), dchess.Engine(0)]
+    engs = [engine] + others
+    jobs = [(s, want_s, 9), (mid, want_mid, 10), (s, want_s, 11)]
+    total = sum(n for _, _, n in jobs)
+    buf = engine.alloc(total * W * 8)
+    try:
+        for e, (p, _, n) in zip(engs, jobs):  # captures first (a plain run per context)
+            e.perft_repeat_device(p, 6, 3, 0, 1, 1, buf)
+            e.synchronize()
+        k0 = 0
+        for e, (p, _, n) in zip(engs, jobs):
+            e.perft_repeat_device(p, 6, 3, 0, 1, n, int(buf.ptr.value) + k0 * W * 8)
+            k0 += n
+        for e in engs:
+            e.synchronize()
+        res = buf.download(np.uint64, total * W).reshape(total, W)
+    finally:
+        buf.free()
+        for e in others:
+            e.close()
+    want = np.concatenate([np.full(n, w, np.uint64) for _, w, n in jobs])
+    assert (res[:, 257] == want).all(), res[:, 257]
+    assert not (res[:, 256] >> np.uint64(32)).any()
+
+
 def test_perft_repeat_device_profiling_then_other_position(engine):
     """With profiling on, dc_perft_repeat_device enqueues plain (non-graph) runs,
     each copying the pinned root block when it executes; a perft of another
