@@ -1214,7 +1214,16 @@ struct alignas(16) C2cRec {
 // the 48-byte records so that four blocks' LDS (<= 40,960 B each) fit a CU;
 // 19.9 with the 56-byte records and the second queue (the mean at perft(7) is
 // 7.6: 0.306 of 24.7 children).
-constexpr u32 kC2cCap = DC_C2C_REC ? (DC_C2C_DIAGQ ? 5104 : 6128) : 256 * 24;
+// DC_C2C_QQ (round 5, with the group-wise queue): the quiet special children
+// (after the target-side pawn correction: 1.7 % of perft(7)'s children, 11 %
+// of the enumerated ones) go to a third per-wave queue and get their pawn
+// recount 64 at a time, instead of the whole wave running it in nearly every
+// consume round; their 512 queue slots come out of the slot area (19.9 -> 17.9
+// per parent; 3.9 special children per parent on average since the correction).
+#ifndef DC_C2C_QQ
+#define DC_C2C_QQ DC_C2C_DIAGQ
+#endif
+constexpr u32 kC2cCap = DC_C2C_REC ? (DC_C2C_DIAGQ ? (DC_C2C_QQ ? 5104 - 4 * kC2cQueue : 5104) : 6128) : 256 * 24;
 
 template <u32 CAP>
 struct C2cShared {
@@ -1230,8 +1239,11 @@ struct C2cShared {
 #if DC_C2C_DIAGQ
   u32 queue_d[4][kC2cQueue];
 #endif
+#if DC_C2C_QQ
+  u32 queue_q[4][kC2cQueue];
+#endif
   u64 hist[256];
-  u64 wsum[4];
+  u64 wsum[6];  // scans; the pooled final drains' per-wave leftovers (12 u32)
   u32 next;
 #if !DC_C2C_REC
   uint16_t ptag[256];
@@ -1335,6 +1347,14 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
 #else
   u32* qd = q;
 #endif
+  // QQ: the quiet special children's queue (their pawn recount, 64 at a time)
+  constexpr bool QQ = DC_C2C_QQ && GQ;
+#if DC_C2C_QQ
+  u32* qq = sh.queue_q[w];
+#else
+  u32* qq = q;
+#endif
+  u32 qnq = 0;
   u32 cnt = 0, base = 0, diag = 0;
   u64 att = 0, orth = 0, Fs = 0, Ts = 0, simple_leaves = 0;
   u32 nsim = 0;
@@ -1399,7 +1419,13 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     const int f = (int)(c.e & 63), t = (int)((c.e >> 6) & 63);
     const u64 occ = occupied(c.pb);
     const bool quiet = ((((occ | c.a) >> t) | (c.a >> f)) & 1) == 0;
-    if (live && quiet) add_tag(c.tag, c.base + (PHASE == 6 ? (u32)t : ref_pawn_count_child<1 - STM>(c.pb, f, t)), true);
+    if constexpr (QQ) {
+      const u64 qmask = ballot(live && quiet);
+      if (live && quiet) qq[qnq + mask_rank(qmask)] = c.e;
+      qnq = __builtin_amdgcn_readfirstlane(qnq + (u32)__popcll(qmask));
+    } else {
+      if (live && quiet) add_tag(c.tag, c.base + (PHASE == 6 ? (u32)t : ref_pawn_count_child<1 - STM>(c.pb, f, t)), true);
+    }
     const bool full = live && !quiet;
     const u64 em = ballot(full);
     if constexpr (PHASE == 7) {  // statistics: divide[0] quiet special children, [1] full-recount children
@@ -1468,9 +1494,25 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     qnd = __builtin_amdgcn_readfirstlane(qnd - 64);
 #endif
   };
+  // one quiet child: base + O's pawn moves in the child (the record's board)
+  auto quiet_count = [&](u32 e2) -> u32 {
+    const u32 pl = e2 >> 15;
+    const int f = (int)(e2 & 63), t = (int)((e2 >> 6) & 63);
+    return sh.basec(pl) + (PHASE == 6 ? (u32)t : ref_pawn_count_child<1 - STM>(sh.board(pl), f, t));
+  };
+  auto drain64q = [&]() {  // qnq >= 64: 64 queued quiet children
+    wave_lds_sync();
+    const u32 e2 = qq[lane];
+    const u32 tg = sh.tag(e2 >> 15);
+    add_tag(tg, quiet_count(e2), true);
+    wave_lds_sync();
+    if (lane + 64 < qnq) qq[lane] = qq[lane + 64];
+    qnq = __builtin_amdgcn_readfirstlane(qnq - 64);
+  };
   auto drain = [&]() {
     if (qn >= 64) drain64();
     if constexpr (GQ) if (qnd >= 64) drain64d();
+    if constexpr (QQ) if (qnq >= 64) drain64q();
   };
   if constexpr (BULK && PHASE != 7) add(otid(w), (u32)simple_leaves, valid);
   if constexpr (PHASE == 7) {  // [2] simple children, [3] parents
@@ -1556,38 +1598,45 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
   // (the partial final drains were 15 % of k_count3c's VALU issue cycles,
   // tools/bbprof_inline.py).  The parents' records are still in LDS.
   {
-    u32* cnt = reinterpret_cast<u32*>(sh.wsum);  // [0..3] full, [4..7] group-wise (the scan is done)
+    // [0..3] full, [4..7] group-wise, [8..11] quiet (the scan is done)
+    u32* cnt = reinterpret_cast<u32*>(sh.wsum);
     __syncthreads();  // every wave is past its last slot read: the slot area is free
     if (lane == 0) {
       cnt[w] = qn;
       cnt[4 + w] = GQ ? qnd : 0u;
+      cnt[8 + w] = QQ ? qnq : 0u;
     }
     __syncthreads();
-    u32 of = 0, od = 0, nf = 0, nd = 0;
+    u32 of = 0, od = 0, oq = 0, nf = 0, nd = 0, nq = 0;
 #pragma unroll
     for (u32 v = 0; v < 4; ++v) {
-      const u32 a = cnt[v], b = cnt[4 + v];
+      const u32 a = cnt[v], b = cnt[4 + v], x = cnt[8 + v];
       of += v < w ? a : 0u;
       od += v < w ? b : 0u;
+      oq += v < w ? x : 0u;
       nf += a;
       nd += b;
+      nq += x;
     }
     nf = __builtin_amdgcn_readfirstlane(nf);
     nd = __builtin_amdgcn_readfirstlane(nd);
+    nq = __builtin_amdgcn_readfirstlane(nq);
     if (lane < qn) sh.slot[of + lane] = q[lane];
     if (GQ && lane < qnd) sh.slot[nf + od + lane] = qd[lane];
+    if (QQ && lane < qnq) sh.slot[nf + nd + oq + lane] = qq[lane];
     __syncthreads();
-    const u32 cf = (nf + 63) / 64, cd = (nd + 63) / 64;
-    for (u32 c = w; c < cf + cd; c += 4) {
-      const bool full = c < cf;  // wave-uniform
-      const u32 k = (full ? c * 64 : nf + (c - cf) * 64) + lane;
-      const bool live = k < (full ? nf : nf + nd);
+    const u32 cf = (nf + 63) / 64, cd = (nd + 63) / 64, cq = (nq + 63) / 64;
+    for (u32 c = w; c < cf + cd + cq; c += 4) {
+      const u32 kind = c < cf ? 0u : c < cf + cd ? 1u : 2u;  // wave-uniform
+      const u32 k = (kind == 0 ? c * 64 : kind == 1 ? nf + (c - cf) * 64 : nf + nd + (c - cf - cd) * 64) + lane;
+      const bool live = k < (kind == 0 ? nf : kind == 1 ? nf + nd : nf + nd + nq);
       const u32 e2 = live ? sh.slot[k] : 0u;
       u32 r = 0;
-      if (full) r = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2)) : 0u;
+      if (kind == 0) r = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_full<STM>(sh, e2)) : 0u;
 #if DC_C2C_DIAGQ
-      else r = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_diag<STM>(sh, e2)) : 0u;
+      else if (kind == 1) r = live ? (PHASE == 5 || PHASE == 6 ? e2 & 1 : c2c_diag<STM>(sh, e2)) : 0u;
 #endif
+      else if (QQ) r = live ? quiet_count(e2) : 0u;
       add(e2 >> 15, r, live);
     }
   }
@@ -1609,6 +1658,12 @@ __device__ __forceinline__ void c2c_group(C2cShared<CAP>& sh, bool valid, const 
     add(e2 >> 15, k, live);
   }
 #endif
+  if (QQ && qnq) {
+    wave_lds_sync();
+    const bool live = lane < qnq;
+    const u32 e2 = live ? qq[lane] : 0u;
+    add(e2 >> 15, live ? quiet_count(e2) : 0u, live);
+  }
 #endif
   tag_hist_add(sh.hist, tag0, acc, true);
   __syncthreads();  // par/att/ptag/slot reused by the next group
