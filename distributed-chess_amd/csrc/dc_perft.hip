@@ -953,6 +953,7 @@ struct C2bShared : C2bSens<SPLIT> {
   u64 hist[256];
   u64 wsum[4];
   uint16_t ptag[256];
+  u32 next;  // the chunk this block takes next (dynamic scheduling)
 };
 static_assert(sizeof(C2bShared<false>) + sizeof(u64) * SN_COUNT * 256 == sizeof(C2bShared<true>) +
                   sizeof(u32) * (C2bCfg<false>::kCap - C2bCfg<true>::kCap),
@@ -981,10 +982,18 @@ extern "C" __attribute__((visibility("default"))) int dc_diag_child_set(void* de
 }
 #endif
 
+// DC_C2B_DYN (round 5): blocks take 256-parent chunks from a counter (the run's
+// PerftResult.next_chunk, zeroed by k_expand_top) instead of an equal static
+// share: a parent's cost varies several-fold, and with a handful of chunks per
+// block (the FIDE suite's one batched final stage: 938 chunks over 768 blocks)
+// the static split left most CUs idle behind the slowest blocks.
+#ifndef DC_C2B_DYN
+#define DC_C2B_DYN 1
+#endif
 template <class R, int STM>
 __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
-                                                    u64* __restrict__ divide) {
+                                                    u64* __restrict__ divide, u32* __restrict__ next_chunk) {
   constexpr bool SPLIT = R::kSplit;
   constexpr u32 kC2bCap = C2bCfg<SPLIT>::kCap;
   __shared__ C2bShared<SPLIT> sh;
@@ -994,12 +1003,28 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
   // Equal contiguous share of the level per resident block (the grid is one
   // resident wave of blocks, so every CU carries the same number of parents).
   const u64 lo = rng->lo, hi = rng->hi;
-  const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;
+#if DC_C2B_DYN && !defined(DC_DIAG_CHILD)
+  // chunks of up to 256 parents; a level with fewer than 256 per block (the
+  // suite's single positions: 3k-100k parents over 768 blocks) takes smaller
+  // ones, so every block still gets work, as the static split gave it
+  const u64 cs = min<u64>(kChunk, max<u64>(1, (hi - lo + gridDim.x - 1) / gridDim.x));
+  const u64 nch = (hi - lo + cs - 1) / cs;
+  for (;;) {
+    if (tid == 0) sh.next = atomicAdd(next_chunk, 1u);
+    __syncthreads();
+    const u64 c = sh.next;
+    if (c >= nch) break;  // block-uniform
+    const u64 s = lo + c * cs;
+    const u64 bhi = min(hi, s + cs);
+#else
+  (void)next_chunk;
+  const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;  // (DC_C2B_DYN=0, and the diagnostic builds)
   const u64 blo = min(hi, lo + (u64)blockIdx.x * per), bhi = min(hi, blo + per);
 #ifdef DC_DIAG_CHILD
   u64 diag_off = (u64)blockIdx.x * per * 218;  // 218: the most legal moves of any position
 #endif
   for (u64 s = blo; s < bhi; s += kChunk) {
+#endif
     const u64 i = s + tid;
     const bool valid = i < bhi;
     Board p{0, 0, 0, 0};
@@ -2251,6 +2276,9 @@ hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const u
 // k_count2 and k_count2b<RefRules> are compiled only into the A/B build.
 hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Board* nodes, const uint16_t* meta,
                         const uint16_t* tags, const Range* rng, u64 n_bound, u64* divide, const PerftResult* res) {
+  // divide is the run's PerftResult.divide (its first member): k_count2b's chunk counter sits in the same block
+  static_assert(offsetof(PerftResult, divide) == 0, "divide heads the result block");
+  u32* next_chunk = &reinterpret_cast<PerftResult*>(divide)->next_chunk;
   if (plies == 1) {
     DC_LAUNCH_RULES_STM(k_count1, grid_for(n_bound, 256), 256, st, nodes, meta, tags, rng, divide);
     return hipGetLastError();
@@ -2261,14 +2289,14 @@ hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Boa
     return hipGetLastError();
   }
   if (rules == 0 && final_variant() == 0) {
-    DC_LAUNCH_STM(k_count2b, RefRules, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
+    DC_LAUNCH_STM(k_count2b, RefRules, kMaxGrid, 256, st, nodes, meta, tags, rng, divide, next_chunk);
     return hipGetLastError();
   }
 #else
   (void)res;
 #endif
   if (rules == 0) launch_count2c(st, stm, nodes, tags, rng, divide);
-  else DC_LAUNCH_STM(k_count2b, FideRules, kMaxGrid, 256, st, nodes, meta, tags, rng, divide);
+  else DC_LAUNCH_STM(k_count2b, FideRules, kMaxGrid, 256, st, nodes, meta, tags, rng, divide, next_chunk);
   return hipGetLastError();
 }
 
