@@ -1004,16 +1004,17 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
   // resident wave of blocks, so every CU carries the same number of parents).
   const u64 lo = rng->lo, hi = rng->hi;
 #if DC_C2B_DYN && !defined(DC_DIAG_CHILD)
-  // chunks of up to 256 parents; a level with fewer than 256 per block (the
-  // suite's single positions: 3k-100k parents over 768 blocks) takes smaller
-  // ones, so every block still gets work, as the static split gave it
-  const u64 cs = min<u64>(kChunk, max<u64>(1, (hi - lo + gridDim.x - 1) / gridDim.x));
+  // chunks of min(256, the block's equal share): a level of < 256 parents a
+  // block (the suite's single positions) one chunk per block, as the static
+  // split had it.  Each block's first chunk is its own index (no atomic round
+  // trip at the start: that alone cost the single suite positions 4-9 %); the
+  // counter hands out the rest from gridDim.x on.  (Chunks of a quarter share
+  // for mid-size levels measured slower on the suite batch: 0.426 vs 0.418 ms,
+  // profiles/r05/ab_z2.jsonl.)
+  const u64 share = max<u64>(1, (hi - lo + gridDim.x - 1) / gridDim.x);
+  const u64 cs = min<u64>(kChunk, share);
   const u64 nch = (hi - lo + cs - 1) / cs;
-  for (;;) {
-    if (tid == 0) sh.next = atomicAdd(next_chunk, 1u);
-    __syncthreads();
-    const u64 c = sh.next;
-    if (c >= nch) break;  // block-uniform
+  for (u64 c = blockIdx.x; c < nch;) {  // block-uniform
     const u64 s = lo + c * cs;
     const u64 bhi = min(hi, s + cs);
 #else
@@ -1153,6 +1154,11 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
 #endif
     tag_hist_add(sh.hist, tag0, acc, true);
     __syncthreads();  // par/ptag/slot reused by the next chunk
+#if DC_C2B_DYN && !defined(DC_DIAG_CHILD)
+    if (tid == 0) sh.next = gridDim.x + atomicAdd(next_chunk, 1u);
+    __syncthreads();
+    c = sh.next;
+#endif
   }
   tag_hist_flush(sh.hist, divide);
 }
