@@ -1812,17 +1812,15 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
 #if DC_C3C_STATIC
   u32 k_static = 0;  // A/B diagnostics: block b takes groups b, b + grid, ... (no counter)
 #endif
+  // Each block's first group is its own index (round 5: no atomic round trip
+  // before the first load, as in k_count2b); the counter hands out the rest
+  // from gridDim.x on.
+  u32 grp = blockIdx.x;
   for (;;) {
     // (fetching the next group's index one group ahead, to take its round
     // trip off the load chain, made the kernel 0.495 -> 0.519 ms at perft(7):
     // a block then holds a group it cannot start, which lengthens the tail)
-#if DC_C3C_STATIC
-    if (t0) sh.next = blockIdx.x + (k_static++) * gridDim.x;
-#else
-    if (t0) sh.next = atomicAdd(next_group, 1u);
-#endif
-    __syncthreads();
-    const u64 s = (u64)sh.next * kGroup;
+    const u64 s = (u64)grp * kGroup;
     if (s >= total) break;  // block-uniform
     const u64 i = s + otid(wave);
     const bool valid = i < total;
@@ -1840,8 +1838,8 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
 #if DC_C3C_LOG
     // diagnostics: the block's cumulative histogram after each group
     // (read back by dc_ab_c3c_log; tools/c2c_groups.py takes differences)
-    if (sh.next < kC3cLogGroups) {
-      u64* rec = g_c3c_log + (u64)sh.next * kC3cLogWords;
+    if (grp < kC3cLogGroups) {
+      u64* rec = g_c3c_log + (u64)grp * kC3cLogWords;
       const u32 tid = otid(wave);
       rec[tid] = sh.hist[tid];
       if (tid == 0) {
@@ -1851,6 +1849,14 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
     }
     __syncthreads();
 #endif
+    // (c2c_group ended with a barrier: every thread is past its read of grp's state)
+#if DC_C3C_STATIC
+    if (t0) sh.next = blockIdx.x + (++k_static) * gridDim.x;
+#else
+    if (t0) sh.next = gridDim.x + atomicAdd(next_group, 1u);
+#endif
+    __syncthreads();
+    grp = sh.next;
   }
   tag_hist_flush(sh.hist, divide, otid(wave));
 }
