@@ -1723,11 +1723,13 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
   // Blocks take 256-parent chunks from a counter: the cost of a chunk varies
   // with its positions, and static ranges left the slowest block behind (a
   // sharded launch has only ~3 chunks per block).  The counter's round trips
-  // are 2.7 % of a block's lifetime at perft(7) (tools/c2c_trace.py).
-  for (;;) {
+  // are 2.7 % of a block's lifetime at perft(7) (tools/c2c_trace.py).  Each
+  // block's first chunk is its own index (round 5, as k_count3c): the counter
+  // hands out the rest from gridDim.x on.
+  for (bool first = true;; first = false) {
     [[maybe_unused]] u64 ta = 0;
     if constexpr (PHASE == 8) ta = wall_clock64();
-    if (t0) sh.next = atomicAdd(next_chunk, 1u);
+    if (t0) sh.next = first ? blockIdx.x : gridDim.x + atomicAdd(next_chunk, 1u);
     __syncthreads();
     if constexpr (PHASE == 8) {
       t_last = wall_clock64();
