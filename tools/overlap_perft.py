@@ -27,7 +27,7 @@ if a.torch:
     assert torch.cuda.is_available()
     torch.cuda.synchronize()
 W = 258
-WANT = {6: 120909581, 7: 3282734510}  # REF
+WANT = {6: 120909581, 7: 3282734510, 8: 88792516787}  # REF
 pos = dchess.startpos()
 engs = [dchess.Engine(0) for _ in range(a.ctx)]
 bufs = [e.alloc(a.steps * W * 8) for e in engs]
