@@ -21,6 +21,7 @@ ap.add_argument("--depth", type=int, default=7)
 ap.add_argument("--ctx", type=int, default=2)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--torch", action="store_true", help="initialise torch's HIP runtime first (as bench.py does)")
+ap.add_argument("--shards", type=int, default=1, help="time shard 0 of N (one rank's work at N GPUs)")
 a = ap.parse_args()
 if a.torch:
     import torch
@@ -33,26 +34,29 @@ engs = [dchess.Engine(0) for _ in range(a.ctx)]
 bufs = [e.alloc(a.steps * W * 8) for e in engs]
 for e, b in zip(engs, bufs):
     for k in (1, 8, a.steps // a.ctx):
-        e.perft_repeat_device(pos, a.depth, 3, 0, 1, k, b)
+        e.perft_repeat_device(pos, a.depth, 3, 0, a.shards, k, b)
     e.synchronize()
 
 
 def check(b, n):
     r = b.download(np.uint64, n * W).reshape(n, W)
-    assert (r[:, 257] == WANT[a.depth]).all(), r[:, 257][:4]
+    if a.shards == 1:
+        assert (r[:, 257] == WANT[a.depth]).all(), r[:, 257][:4]
+    else:  # one shard: every run the same count
+        assert (r[:, 257] == r[0, 257]).all() and r[0, 257] > 0, r[:, 257][:4]
 
 
-out = {"depth": a.depth, "steps": a.steps, "ctx": a.ctx, "torch": a.torch, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
+out = {"depth": a.depth, "steps": a.steps, "ctx": a.ctx, "torch": a.torch, "shards": a.shards, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES")}
 for rep in range(a.reps):
     t0 = time.perf_counter()
-    engs[0].perft_repeat_device(pos, a.depth, 3, 0, 1, a.steps, bufs[0])
+    engs[0].perft_repeat_device(pos, a.depth, 3, 0, a.shards, a.steps, bufs[0])
     engs[0].synchronize()
     one = time.perf_counter() - t0
     check(bufs[0], a.steps)
     share = a.steps // a.ctx
     t0 = time.perf_counter()
     for i, (e, b) in enumerate(zip(engs, bufs)):
-        e.perft_repeat_device(pos, a.depth, 3, 0, 1, share, b)
+        e.perft_repeat_device(pos, a.depth, 3, 0, a.shards, share, b)
     for e in engs:
         e.synchronize()
     many = time.perf_counter() - t0
