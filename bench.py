@@ -227,18 +227,21 @@ def perft_contexts(eng, d, n):
     return [eng] + extra[:n - 1]
 
 
-def perft_streams(args, depth):
+def perft_streams(args, depth, world=1):
     """Contexts a repeated perft(depth) is spread over.  One perft's front end
     (the one-workgroup top expansion and the level chain before the final stage,
     ~70 us) is latency-bound; with the steps split over two or three contexts --
     streams -- one run's front end executes while another's final stage holds
     the CUs (tools/overlap_perft.py, profiles/r05/overlap_u.jsonl: perft(7)
-    0.408 -> 0.378 ms per step with 2, perft(6) 0.068 -> 0.034 with 3).  Every
-    step is still a whole perft with its own result record.  Deep runs (the
-    final stage is everything) keep one."""
+    0.408 -> 0.378 ms per step with 2, perft(6) 0.068 -> 0.034 with 3).  A rank
+    of N >= 4 holds a shard whose final stage is shorter than the front end, so
+    perft(7) takes 3 there (shard 0 of 8: 0.116 ms on one context, 0.070 on
+    two, 0.062 on three; profiles/r05/overlap_ab_shards.jsonl).  Every step is
+    still a whole perft (of this rank's shard) with its own result record.  Deep
+    runs (the final stage is everything) keep one."""
     if args.perft_streams:
         return args.perft_streams
-    return 3 if depth <= 6 else 2 if depth == 7 else 1
+    return 3 if depth <= 6 else (3 if world >= 4 else 2) if depth == 7 else 1
 
 
 def enqueue_split(engs, steps, base_ptr, W, fn):
@@ -276,7 +279,7 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF,
     # the first dc_perft_repeat_device call of a configuration runs one plain
     # perft and captures the launch graphs (one run, and a batch of
     # REPEAT_BATCH runs): do it here, outside the timed region
-    engs = perft_contexts(eng, d, max(1, min(perft_streams(args, depth), steps)))
+    engs = perft_contexts(eng, d, max(1, min(perft_streams(args, depth, d.world), steps)))
     share = -(-steps // len(engs))
     warm = eng.alloc(REPEAT_BATCH * W * 8)
     for e in engs:  # every context captures its graphs (one run; a batch of REPEAT_BATCH when its share has one)
@@ -1022,7 +1025,7 @@ def main():
         l6, dt6 = timed_perft(eng, d, args, pos, 6, 4 * args.steps, args.warmup)
         p6 = {"value": l6 / dt6, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt6 / (4 * args.steps),
               "steps": 4 * args.steps, "workload": "perft(startpos, 6) RULES_REF, frontier split at ply 3",
-              "scaling": "strong", "streams_per_gpu": perft_streams(args, 6)}
+              "scaling": "strong", "streams_per_gpu": perft_streams(args, 6, d.world)}
     if "perft8" in legs:
         note("perft8")
         p8 = perft8_leg(eng, d, args, pos)
@@ -1071,7 +1074,7 @@ def main():
                                "per-root-move counts all-reduced over RCCL",
                    "depth": args.depth, "rules": "REF", "leaves_per_step": REF_STARTPOS.get(args.depth),
                    "parallelism": f"dp{d.world}",
-                   "streams_per_gpu": perft_streams(args, args.depth),
+                   "streams_per_gpu": perft_streams(args, args.depth, d.world),
                    "streams_note": "the K timed steps are split over this many contexts (HIP streams) per GPU, "
                                    "each enqueuing its share at once; each step is a whole perft with its own "
                                    "result record, and one run's latency-bound front end overlaps another's "
