@@ -1465,7 +1465,12 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   };
   // The target ply of k_expand_top is made on many CUs by k_make_count (it
   // replaces that level's k_level_count) when that level is counted next.
-  bool top_words = !exact && T >= 2 && T < F && !(sharded && S == T);
+  // A rank's strided shard of that ply (round 5): the words stay whole and
+  // k_make_count makes only this rank's (word shard + i x n_shards), instead
+  // of the one workgroup making the whole ply as boards and k_gather_shard
+  // copying the shard out of it.
+  const bool shard_words = !exact && sharded && S == T && T >= 2 && T < F && !shard_contiguous();
+  bool top_words = !exact && T >= 2 && T < F && (!(sharded && S == T) || shard_words);
   if (top_words) HIP_TRY(c->top_words.ensure(cap_T));
   // the result block is cleared by k_expand_top itself (its first stores)
   HIP_TRY(c->timed("expand_top", 0, [&] {
@@ -1491,7 +1496,8 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
     return DC_SUCCESS;
   };
   if (sharded && L == S) {
-    e = take_shard();
+    if (shard_words) HIP_TRY(dc::launch_shard_range(c->stream, c->rng.p + L, shard, n_shards));
+    else e = take_shard();
     if (e != DC_SUCCESS) return e;
   }
   // Level L's counts and chunk sums live in buffer pair cb; the k_level_write
@@ -1518,7 +1524,8 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
       HIP_TRY(c->timed("expand_count", 0, [&] {
         return dc::launch_make_count(c->stream, rules, stm ^ 1, ts.nodes[T - 2], ts.meta[T - 2], ts.tags[T - 2],
                                      c->top_words.p, c->rng.p + L, nb, c->nodes[buf].p,
-                                     fide ? c->meta[buf].p : nullptr, c->tags[buf].p, cnt_buf[cb]->p, sum_buf[cb]->p);
+                                     fide ? c->meta[buf].p : nullptr, c->tags[buf].p, cnt_buf[cb]->p, sum_buf[cb]->p,
+                                     shard_words ? shard : 0u, shard_words ? n_shards : 1u);
       }));
     } else if (!counted) {
       HIP_TRY(c->timed("expand_count", 0, [&] {

@@ -42,9 +42,16 @@ hipError_t launch_expand_top(hipStream_t st, u32 rules, const Board* root, const
 // move words {parent << 15 | f | t << 6 | promo << 12} over the previous top
 // ply (s.nodes[target - 2]); launch_make_count then makes, stores and counts
 // it (in place of launch_level_count).  stm_par = side to move at the parents.
+// wsh / wstride (a rank's strided shard of the word level, round 5): child i of
+// the made level is word wsh + i * wstride; the level's Range is the shard's
+// (launch_shard_range).
 hipError_t launch_make_count(hipStream_t st, u32 rules, int stm_par, const Board* par, const uint16_t* par_meta,
                              const uint16_t* par_tags, const u32* words, const Range* rng, u64 n_bound, Board* out,
-                             uint16_t* out_meta, uint16_t* out_tags, u32* counts, u64* chunk_sum);
+                             uint16_t* out_meta, uint16_t* out_tags, u32* counts, u64* chunk_sum, u32 wsh = 0,
+                             u32 wstride = 1);
+// rng := the size of the strided shard `shard` of n_shards of the level rng
+// (nodes shard, shard + n_shards, ...), as k_gather_shard's, without copying.
+hipError_t launch_shard_range(hipStream_t st, Range* rng, u32 shard, u32 n_shards);
 // Per level: count (+ chunk sums), one-workgroup chunk scan (-> next Range), write.
 u64 chunks_for(u64 n);
 hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* nodes, const uint16_t* meta,

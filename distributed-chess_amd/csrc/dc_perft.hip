@@ -485,7 +485,8 @@ __global__ __launch_bounds__(256) void k_make_count(const Board* __restrict__ pa
                                                     const uint16_t* __restrict__ par_tags, const u32* __restrict__ words,
                                                     const Range* __restrict__ rng, Board* __restrict__ out,
                                                     uint16_t* __restrict__ out_meta, uint16_t* __restrict__ out_tags,
-                                                    u32* __restrict__ counts, u64* __restrict__ chunk_sum) {
+                                                    u32* __restrict__ counts, u64* __restrict__ chunk_sum, u32 wsh,
+                                                    u32 wstride) {
   __shared__ u64 wsum[4];
   const u64 lo = rng->lo, hi = rng->hi;
   const u64 nch = (hi - lo + kChunk - 1) / kChunk;
@@ -493,7 +494,7 @@ __global__ __launch_bounds__(256) void k_make_count(const Board* __restrict__ pa
     const u64 i = lo + c * kChunk + threadIdx.x;
     u32 cnt = 0;
     if (i < hi) {
-      const u32 e = words[i];
+      const u32 e = words[wsh + i * wstride];  // (a strided shard of the word level: wstride > 1)
       const u32 pl = e >> 15;
       Board ch = par[pl];
       const u32 cm = R::template make<STM>(ch, load_meta<R>(par_meta, pl), (int)(e & 63), (int)((e >> 6) & 63),
@@ -2048,10 +2049,22 @@ hipError_t launch_level_count(hipStream_t st, u32 rules, int stm, const Board* n
 
 hipError_t launch_make_count(hipStream_t st, u32 rules, int stm_par, const Board* par, const uint16_t* par_meta,
                              const uint16_t* par_tags, const u32* words, const Range* rng, u64 n_bound, Board* out,
-                             uint16_t* out_meta, uint16_t* out_tags, u32* counts, u64* chunk_sum) {
+                             uint16_t* out_meta, uint16_t* out_tags, u32* counts, u64* chunk_sum, u32 wsh,
+                             u32 wstride) {
   const int stm = stm_par;
   DC_LAUNCH_RULES_STM(k_make_count, grid_for(n_bound, kChunk), 256, st, par, par_meta, par_tags, words, rng, out,
-                      out_meta, out_tags, counts, chunk_sum);
+                      out_meta, out_tags, counts, chunk_sum, wsh, wstride);
+  return hipGetLastError();
+}
+
+__global__ void k_shard_range(Range* rng, u32 shard, u32 n_shards) {
+  const u64 lo = rng->lo, hi = rng->hi;
+  const u64 n = hi > lo + shard ? (hi - lo - shard + n_shards - 1) / n_shards : 0;  // as k_gather_shard
+  *rng = Range{0, n};
+}
+
+hipError_t launch_shard_range(hipStream_t st, Range* rng, u32 shard, u32 n_shards) {
+  hipLaunchKernelGGL(k_shard_range, dim3(1), dim3(1), 0, st, rng, shard, n_shards);
   return hipGetLastError();
 }
 
