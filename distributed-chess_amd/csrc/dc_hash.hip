@@ -37,6 +37,8 @@
 #include "dc_hash.h"
 #include "dc_keccak.h"
 
+DC_BBPROF_DEFINE(hash)  // measurement builds only (tools/bbprof.py)
+
 namespace dc {
 
 // ----------------------------------------------------------- JSON templates
@@ -100,6 +102,17 @@ __device__ __forceinline__ u32 kind_index(u32 code) {
 constexpr u32 kHashThreads = 256;
 constexpr u32 kTokBytes = 16;
 constexpr u32 kAccPlies = 128;  // per-lane verdict bits kept from pass 1 (4 dwords of LDS)
+// DC_HASH_COPY8 (round 5): pieces whose bytes sit in LDS (templates, move
+// tokens) are copied 8 bytes a step -- eight ds_read_u8 then eight ds_write_b8
+// at immediate offsets, one wait -- instead of a generic-pointer byte loop that
+// waits on every byte.  A step may read up to 7 bytes past its piece (LDS: in
+// the block's allocation, or 0 past it) and write up to 7 past the block's
+// byte 135, so each lane's block row is kBlkRow (>= 143) bytes; the bytes
+// written past a piece are overwritten by the next piece or by the padding.
+#ifndef DC_HASH_COPY8
+#define DC_HASH_COPY8 1
+#endif
+constexpr u32 kBlkRow = DC_HASH_COPY8 ? 152 : kKeccakRate;  // 38 dwords: 2-way banks for the u64 absorb reads
 
 // Stages of a lane's JSON stream (in order).
 enum : u32 {
@@ -113,9 +126,12 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
                                                                   u32 hist_tokens, const char* __restrict__ names,
                                                                   const u32* __restrict__ names_off,
                                                                   uint8_t* __restrict__ out) {
-  __shared__ char tpl[sizeof(g_json_tpl.s)];
-  __shared__ __attribute__((aligned(8))) uint8_t blk[kHashThreads][kKeccakRate];
-  __shared__ char tok[kHashThreads][kTokBytes];
+  // templates and the lanes' move tokens in one LDS pool (a piece in LDS is an
+  // offset into it; names and the start history are global pointers)
+  constexpr u32 kTplBytes = sizeof(g_json_tpl.s);
+  __shared__ char lpool[kTplBytes + kHashThreads * kTokBytes];
+  __shared__ __attribute__((aligned(8))) uint8_t blk[kHashThreads][kBlkRow];
+  char* const tpl = lpool;
   __shared__ u32 accb[kAccPlies / 32][kHashThreads];  // [word][lane]: bank per lane
   const u32 tid = threadIdx.x;
   for (u32 i = tid; i < sizeof(g_json_tpl.s); i += kHashThreads) tpl[i] = g_json_tpl.s[i];
@@ -149,7 +165,10 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   Board b = start;
   u32 cur = stm0, ply = 0, ntok = hist_tokens;
   u32 stage = active ? S_TURN : S_DONE;
-  const char* src = tpl + g_json_tpl.off[T_TURN];
+  // the current piece: lpool[loff...] (glb false) or src[...] (glb true)
+  const char* src = nullptr;
+  bool glb = false;
+  u32 loff = g_json_tpl.off[T_TURN];
   u32 rem = active ? g_json_tpl.len[T_TURN] : 0u;
   u32 row = 0, col = 0;
   u32 wn0 = 0, wn1 = 0, bn1 = 0;
@@ -158,10 +177,17 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
     wn1 = names_off[2 * g + 1];
     bn1 = names_off[2 * g + 2];
   }
-  char* mytok = tok[tid];
+  const u32 tok_off = kTplBytes + tid * kTokBytes;
+  char* mytok = lpool + tok_off;
   auto tpl_piece = [&](int i, u32 drop) {
-    src = tpl + g_json_tpl.off[i];
+    glb = false;
+    loff = g_json_tpl.off[i];
     rem = g_json_tpl.len[i] - drop;
+  };
+  auto glb_piece = [&](const char* p, u32 n) {
+    glb = true;
+    src = p;
+    rem = n;
   };
   // The piece after the current one (rem == 0: the stream has ended).
   auto next_piece = [&]() {
@@ -169,15 +195,15 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
       switch (stage) {
         case S_TURN:
           stage = S_DIGIT;
-          src = tpl + g_json_tpl.off[T_DIGITS] + stm;
-          rem = 1;
+          tpl_piece(T_DIGITS, 1);
+          loff += stm;
           break;
         case S_DIGIT: stage = S_WP; tpl_piece(T_WP, 0); break;
-        case S_WP: stage = S_WNAME; src = names + wn0; rem = wn1 - wn0; break;
+        case S_WP: stage = S_WNAME; glb_piece(names + wn0, wn1 - wn0); break;
         case S_WNAME: stage = S_BP; tpl_piece(T_BP, 0); break;
-        case S_BP: stage = S_BNAME; src = names + wn1; rem = bn1 - wn1; break;
+        case S_BP: stage = S_BNAME; glb_piece(names + wn1, bn1 - wn1); break;
         case S_BNAME: stage = S_HIST; tpl_piece(T_HIST, 0); break;
-        case S_HIST: stage = S_HSTART; src = hist; rem = hist_len; break;
+        case S_HIST: stage = S_HSTART; glb_piece(hist, hist_len); break;
         case S_HSTART:
         case S_TOKENS: {
           stage = S_TOKENS;
@@ -193,13 +219,16 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             const bool cap = (occupied(b) >> t) & 1;
             u32 n = 0;
             if (ntok) mytok[n++] = ' ';
-            char dg[10];
-            u32 nd = 0, v = ntok + 1;
-            do {
-              dg[nd++] = (char)('0' + v % 10);
+            // N's decimal digits written last-first straight into the token
+            // (round 4 built them in a dynamically indexed register array:
+            // 29 % of the kernel's issue cycles in tools/bbprof.py's count)
+            u32 v = ntok + 1, nd = 1;
+            for (u32 q = v; q >= 10; q /= 10) ++nd;
+            for (u32 i = nd; i-- > 0;) {
+              mytok[n + i] = (char)('0' + v % 10);
               v /= 10;
-            } while (v);
-            while (nd) mytok[n++] = dg[--nd];
+            }
+            n += nd;
             mytok[n++] = '.';
             mytok[n++] = ' ';
             if (ki != 0) mytok[n++] = "PNBRQK"[ki];
@@ -212,7 +241,8 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             ref_make(b, f, t);
             cur ^= 1;
             ntok += 2;
-            src = mytok;
+            glb = false;
+            loff = tok_off;
             rem = n;
           }
           if (rem == 0) {
@@ -275,8 +305,25 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           continue;
         }
         const u32 n = min(rem, (u32)kKeccakRate - fill);
-        for (u32 k = 0; k < n; ++k) my[fill + k] = (uint8_t)src[k];
-        src += n;
+        if (glb) {
+          for (u32 k = 0; k < n; ++k) my[fill + k] = (uint8_t)src[k];
+          src += n;
+        } else {
+#if DC_HASH_COPY8
+          for (u32 k = 0; k < n; k += 8) {
+            const char* a = lpool + loff + k;
+            uint8_t* d = my + fill + k;
+            char v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = a[j];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) d[j] = (uint8_t)v[j];
+          }
+#else
+          for (u32 k = 0; k < n; ++k) my[fill + k] = (uint8_t)lpool[loff + k];
+#endif
+          loff += n;
+        }
         rem -= n;
         fill += n;
       }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run one workload on the instrumented library (tools/bbprof_build.sh) and
 write the per-block wave-execution counts (tools/bbprof.py model input).
-  DCHESS_LIB=.../build/bb/libdchess_bb.so python tools/bbprof_run.py perft7|fide7|replay|gen OUT.json
+  DCHESS_LIB=.../build/bb/libdchess_bb.so python tools/bbprof_run.py perft7|fide7|replay|gen|hash OUT.json
 The workload's result is checked against its golden value, so an
 instrumentation that changed the kernel's behaviour fails here."""
 import ctypes as C
@@ -18,7 +18,7 @@ import dchess  # noqa: E402
 work, out = sys.argv[1], sys.argv[2]
 reps = int(sys.argv[3]) if len(sys.argv) > 3 else 1
 L = dchess.lib()
-file = "moves" if work in ("replay", "gen") else "perft"
+file = "moves" if work in ("replay", "gen") else "hash" if work == "hash" else "perft"
 fn = getattr(C.CDLL(dchess.LIB_PATH), f"dc_ab_bbprof_{file}")
 fn.argtypes = [C.c_void_p, C.c_int]
 eng = dchess.Engine(0)
@@ -42,6 +42,21 @@ elif work.startswith("perft"):
         if tot != want:
             raise SystemExit(f"perft({depth}) = {tot}, want {want}: the instrumented kernel changed the result")
     res["result"] = int(tot)
+elif work == "hash":  # k_state_hash_ref on the bench's workload; game 0's hash as the check
+    n = 1_000_000
+    d_mv, d_h = eng.alloc(n * 80 * 2), eng.alloc(n * 32)
+    eng.gen_games_device(d_mv, 0x5EED20241022, 0, n, 80, 32)
+    blob, off = dchess.pack_names([(f"white{g}", f"black{g}") for g in range(n)])
+    d_names, d_off = eng.names_device(blob, off)
+    eng.state_hash_device(d_mv, n, 80, d_names, d_off, d_h)
+    eng.synchronize()
+    assert fn(None, 1) == 0
+    for _ in range(reps):
+        eng.state_hash_device(d_mv, n, 80, d_names, d_off, d_h)
+    h0 = bytes(d_h.download(np.uint8, 32)).hex()
+    if not h0.startswith("384ec2c485379b44"):
+        raise SystemExit(f"game 0 hash {h0}: the instrumented kernel changed the result")
+    res["result"] = h0
 elif work in ("replay", "gen"):
     g = json.load(open(os.path.join(REPO, "tests", "golden", "replay_golden.json")))
     n = 1_000_000
