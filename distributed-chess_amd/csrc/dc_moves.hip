@@ -766,8 +766,28 @@ __device__ __forceinline__ u64 gen_ray(const GenTabs& T, int s, u64 occ) {
   return r ^ T.ray[D][b];
 }
 
+// Ray of a direction D that runs to higher squares (N, E, NE, NW) up to and
+// including the first occupied square, without a bit scan: bl ^ (bl - 1) is
+// every square up to bl's lowest bit (all squares when bl = 0).  A south-going
+// ray is the north-going one of the vertically flipped board (rows swapped by
+// flip_rows, s ^ 56); a count does not care which board it was taken on.
+template <int D>
+__device__ __forceinline__ u64 gen_ray_up(const GenTabs& T, int s, u64 occ) {
+  static_assert(D == 0 || D == 2 || D == 4 || D == 6, "a direction to higher squares");
+  const u64 r = T.ray[D][s];
+  const u64 bl = r & occ;
+  return r & (bl ^ (bl - 1));
+}
+
 #ifndef DC_GEN_MINW
 #define DC_GEN_MINW 1
+#endif
+// DC_GEN_POSRAY (round 5): the slot counts take every ray but W through
+// gen_ray_up (S, SW, SE on the flipped board); the round-4 form scanned each
+// ray's first blocker with a 64-bit lsb / msb and read a second table entry,
+// 33 % of the kernel's issue cycles in tools/bbprof.py's count.
+#ifndef DC_GEN_POSRAY
+#define DC_GEN_POSRAY 1
 #endif
 __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
                                                        u32 noise_per_256, uint16_t* __restrict__ out) {
@@ -787,6 +807,9 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
     const u32 flip = stm ? 56u : 0u;
     const Sides sw = sides<0>(w);
     const u64 E = sw.empty, no = sw.notown, occ = sw.occ;
+#if DC_GEN_POSRAY
+    const u64 occF = flip_rows(occ), noF = flip_rows(no);  // the board with its rows swapped
+#endif
     // pawn sources per direction class (ref_count_from_w's pawn terms)
     const u64 S1 = sw.P & sh<-8>(E);
     const u64 S2 = S1 & kRow(1) & sh<-16>(E);
@@ -826,8 +849,14 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
         const bool any = take(rem, sv);
         u32 c = 0;
         if (any) {  // skipped by a wave none of whose games has a j-th such slider
+#if DC_GEN_POSRAY
+          const int sf = sv ^ 56;  // SW / SE are NW / NE of the flipped board
+          c = pc((gen_ray_up<4>(T, sv, occ) | gen_ray_up<6>(T, sv, occ)) & no) +
+              pc((gen_ray_up<4>(T, sf, occF) | gen_ray_up<6>(T, sf, occF)) & noF);
+#else
           const u64 t = gen_ray<4>(T, sv, occ) | gen_ray<5>(T, sv, occ) | gen_ray<6>(T, sv, occ) | gen_ray<7>(T, sv, occ);
           c = pc(t & no);
+#endif
         }
         sl[3 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
@@ -839,8 +868,13 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
         const bool any = take(rem, sv);
         u32 c = 0;
         if (any) {
+#if DC_GEN_POSRAY
+          c = pc((gen_ray_up<0>(T, sv, occ) | gen_ray_up<2>(T, sv, occ) | gen_ray<3>(T, sv, occ)) & no) +
+              pc(gen_ray_up<0>(T, sv ^ 56, occF) & noF);  // S: N of the flipped board
+#else
           const u64 t = gen_ray<0>(T, sv, occ) | gen_ray<1>(T, sv, occ) | gen_ray<2>(T, sv, occ) | gen_ray<3>(T, sv, occ);
           c = pc(t & no);
+#endif
         }
         sl[6 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
@@ -880,10 +914,19 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
     u64 tv = (((S1 & bit) != 0) ? sh<8>(bit) : 0ull) | (((S2 & bit) != 0) ? sh<16>(bit) : 0ull) |
              (((SL & bit) != 0) ? sh<7>(bit) : 0ull) | (((SR & bit) != 0) ? sh<9>(bit) : 0ull);
     u64 tp = ((sw.N & bit) != 0 ? T.kn[fv] : 0ull) | ((sw.K & bit) != 0 ? T.kg[fv] : 0ull);
+#if DC_GEN_POSRAY
+    if ((sw.D & bit) != 0)
+      tp |= gen_ray_up<4>(T, fv, occ) | gen_ray_up<6>(T, fv, occ) |
+            flip_rows(gen_ray_up<4>(T, fv ^ 56, occF) | gen_ray_up<6>(T, fv ^ 56, occF));
+    if ((sw.O & bit) != 0)
+      tp |= gen_ray_up<0>(T, fv, occ) | gen_ray_up<2>(T, fv, occ) | gen_ray<3>(T, fv, occ) |
+            flip_rows(gen_ray_up<0>(T, fv ^ 56, occF));
+#else
     if ((sw.D & bit) != 0)
       tp |= gen_ray<4>(T, fv, occ) | gen_ray<5>(T, fv, occ) | gen_ray<6>(T, fv, occ) | gen_ray<7>(T, fv, occ);
     if ((sw.O & bit) != 0)
       tp |= gen_ray<0>(T, fv, occ) | gen_ray<1>(T, fv, occ) | gen_ray<2>(T, fv, occ) | gen_ray<3>(T, fv, occ);
+#endif
     tv |= tp & no;
     const u64 treal = stm ? flip_rows(tv) : tv;
     const u32 kk = k - dlo;
