@@ -789,6 +789,14 @@ __device__ __forceinline__ u64 gen_ray_up(const GenTabs& T, int s, u64 occ) {
 #ifndef DC_GEN_POSRAY
 #define DC_GEN_POSRAY 1
 #endif
+// DC_GEN_QSLOT (round 5): the queen (REF never adds a piece: at most one from
+// startpos) is one slot counting both ray sets, beside two bishop and two rook
+// slots -- 8 slots for the binary search to sum instead of 9 (2 B + Q, 2 R + Q).
+#ifndef DC_GEN_QSLOT
+#define DC_GEN_QSLOT 1
+#endif
+constexpr int kGenLine = DC_GEN_QSLOT ? 2 : 3;  // slots per slider line kind
+constexpr int kGenSlots = 3 + 2 * kGenLine + (DC_GEN_QSLOT ? 1 : 0);
 __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u64 first_game, u32 n_games, u32 n_plies,
                                                        u32 noise_per_256, uint16_t* __restrict__ out) {
   __shared__ GenTabs T;
@@ -817,7 +825,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
     const u64 SR = sw.P & sh<-9>(sw.enemy & kNotA);
     u32 n = pc(S1) + pc(S2) + pc(SL) + pc(SR);
     // piece slots: (real square << 8) | move count; square 64 = empty slot
-    u32 sl[9];
+    u32 sl[kGenSlots];
     auto take = [](u64& rem, int& sv) {  // next piece of a set: its view square, or -1
       const bool any = rem != 0;
       sv = any ? lsb(rem) : 0;
@@ -842,9 +850,9 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
       n += c;
     }
     {
-      u64 rem = sw.D;
+      u64 rem = DC_GEN_QSLOT ? (sw.D & ~sw.O) : sw.D;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < kGenLine; ++j) {
         int sv;
         const bool any = take(rem, sv);
         u32 c = 0;
@@ -861,9 +869,9 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
         sl[3 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
-      rem = sw.O;
+      rem = DC_GEN_QSLOT ? (sw.O & ~sw.D) : sw.O;
 #pragma unroll
-      for (int j = 0; j < 3; ++j) {
+      for (int j = 0; j < kGenLine; ++j) {
         int sv;
         const bool any = take(rem, sv);
         u32 c = 0;
@@ -876,9 +884,32 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
           c = pc(t & no);
 #endif
         }
-        sl[6 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+        sl[3 + kGenLine + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
+#if DC_GEN_QSLOT
+      {
+        rem = sw.D & sw.O;
+        int sv;
+        const bool any = take(rem, sv);
+        u32 c = 0;
+        if (any) {
+          const int sf = sv ^ 56;
+#if DC_GEN_POSRAY
+          c = pc((gen_ray_up<0>(T, sv, occ) | gen_ray_up<2>(T, sv, occ) | gen_ray<3>(T, sv, occ) |
+                  gen_ray_up<4>(T, sv, occ) | gen_ray_up<6>(T, sv, occ)) & no) +
+              pc((gen_ray_up<0>(T, sf, occF) | gen_ray_up<4>(T, sf, occF) | gen_ray_up<6>(T, sf, occF)) & noF);
+#else
+          (void)sf;
+          const u64 t = gen_ray<0>(T, sv, occ) | gen_ray<1>(T, sv, occ) | gen_ray<2>(T, sv, occ) | gen_ray<3>(T, sv, occ) |
+                        gen_ray<4>(T, sv, occ) | gen_ray<5>(T, sv, occ) | gen_ray<6>(T, sv, occ) | gen_ray<7>(T, sv, occ);
+          c = pc(t & no);
+#endif
+        }
+        sl[kGenSlots - 1] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+        n += c;
+      }
+#endif
     }
     if (over) n = 0;
     over = n == 0;
@@ -896,7 +927,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
       const u64 mv = stm ? flip_rows(mr) : mr;
       u32 d = pc(S1 & mv) + pc(S2 & mv) + pc(SL & mv) + pc(SR & mv);
 #pragma unroll
-      for (int j = 0; j < 9; ++j) d += (sl[j] >> 8) <= x ? (sl[j] & 0xFF) : 0u;
+      for (int j = 0; j < kGenSlots; ++j) d += (sl[j] >> 8) <= x ? (sl[j] & 0xFF) : 0u;
       if (d <= k) {
         lo = x + 1;
         dlo = d;
