@@ -112,6 +112,11 @@ constexpr u32 kAccPlies = 128;  // per-lane verdict bits kept from pass 1 (4 dwo
 #ifndef DC_HASH_COPY8
 #define DC_HASH_COPY8 1
 #endif
+// DC_HASH_FUSE (round 5): a piece fetched in the fill loop is copied in the
+// same trip (round 4 spent one trip on the fetch and the next on the copy).
+#ifndef DC_HASH_FUSE
+#define DC_HASH_FUSE 1
+#endif
 constexpr u32 kBlkRow = DC_HASH_COPY8 ? 152 : kKeccakRate;  // 38 dwords: 2-way banks for the u64 absorb reads
 
 // Stages of a lane's JSON stream (in order).
@@ -301,8 +306,12 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
       u32 fill = 0;
       while (fill < (u32)kKeccakRate && stage != S_DONE) {
         if (rem == 0) {
-          next_piece();
+          next_piece();  // the next non-empty piece, or the stream's end
+#if DC_HASH_FUSE
+          if (stage == S_DONE) break;  // (the fetch falls through to the copy: one loop trip per piece)
+#else
           continue;
+#endif
         }
         const u32 n = min(rem, (u32)kKeccakRate - fill);
         if (glb) {

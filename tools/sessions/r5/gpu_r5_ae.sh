@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-5 session AE: the state hash's 8-byte LDS piece copy (DC_HASH_COPY8).
+# Round-5 session AE: state-hash A/B against build/abq/hash_off (DC_HASH_COPY8, later DC_HASH_FUSE).
 # State-hash parity first, then the bench's hash leg alternating builds.
 O=gpurun_out/r5
 mkdir -p $O
