@@ -637,6 +637,8 @@ def state_hash_leg(eng, d, args):
     eng.set_profiling(False)
     k = eng.kernel_stats("state_hash")
     kms = k["total_ms"] / max(k["launches"], 1)
+    kp = eng.kernel_stats("state_hash_replay")  # the replay kernel's per-ply info pass before it (round 5)
+    pre_ms = kp["total_ms"] / max(kp["launches"], 1) if kp.get("launches") else 0.0
     rec = _pmc("state_hash") if d.world == 1 else None
     roof = valu_roof("k_state_hash_ref", n / (kms / 1e3), "game", None, rec) if rec else None
     if roof is not None:
@@ -650,9 +652,11 @@ def state_hash_leg(eng, d, args):
     return {"value": total / dt, "unit": "game state hashes/s", "scaling": "weak",
             "workload": f"{n} seeded games x {plies} ply slots per rank: replay + serde_json(GameState) + keccak256 "
                         "per game (names white<g>/black<g>, start history \"\")",
-            "ms_per_step": 1e3 * dt / args.hash_steps, "kernel_avg_ms": kms, "roofline": roof,
+            "ms_per_step": 1e3 * dt / args.hash_steps, "kernel_avg_ms": kms, "replay_prepass_ms": pre_ms,
+            "roofline": roof,
             "note": "inputs resident in HBM (moves, raw UTF-8 names); per call: device-side serde_json escaping of the "
-                    "names (k_escape_len, scan, k_escape_write, one 8-byte readback) + the hash kernel",
+                    "names (k_escape_len, scan, k_escape_write, one 8-byte readback), the replay kernel's per-ply info "
+                    "pass (replay_prepass_ms) + the hash kernel (kernel_avg_ms)",
             "first_hash": "0x" + bytes(h0).hex()}
 
 

@@ -182,7 +182,7 @@ struct dc_ctx {
   DBuf<DevPos> pos;
   DBuf<uint16_t> moves;
   DBuf<uint8_t> verdicts, info;
-  DBuf<uint8_t> replay_info;  // dc_replay_info: ply-major [n_plies][n_games] move info
+  DBuf<uint8_t> replay_info;  // dc_replay_info / the state hash's first pass: ply-major [n_plies][n_games] move info
   DBuf<char> hash_text;    // escaped start history | escaped names of dc_state_hash*
   DBuf<u32> hash_off;      // the names' escaped offsets into hash_text
   DBuf<u32> esc_lens;      // device escaping scratch: per-name escaped lengths,
@@ -1076,9 +1076,27 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
   if (e != DC_SUCCESS) return e;
   const Board b{s0.bb[0], s0.bb[1], s0.bb[2], s0.bb[3]};
   const char* text = c->hash_text.p;
+  // The replay kernel first (round 5): its per-ply info byte (dc_replay_info's
+  // form) gives the hash kernel each ply's verdict, mover kind and capture, so
+  // the hash kernel validates nothing.  Batches past the replay kernel's one
+  // buffer descriptor keep the hash kernel's own validation pass.
+  const uint8_t* d_info = nullptr;
+#ifndef DC_HASH_PRE
+#define DC_HASH_PRE 1  // (0: the round-4 single kernel, for A/B only)
+#endif
+  if (DC_HASH_PRE && n_plies > 0 && (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull) {
+    HIP_TRY(c->replay_info.ensure((size_t)n_games * n_plies));
+    HIP_TRY(c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(n_games)));
+    bool host_written = false;
+    HIP_TRY(c->timed("state_hash_replay", (u64)n_games * n_plies, [&] {
+      return dc::launch_replay_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, nullptr, nullptr, c->stats5.p,
+                                   c->stats5.p + 5, nullptr, &host_written, c->replay_info.p);
+    }));
+    d_info = c->replay_info.p;
+  }
   HIP_TRY(c->timed("state_hash", n_games, [&] {
     return dc::launch_state_hash_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, text, hist_len, hist_tokens,
-                                     text, c->hash_off.p, d_hashes);
+                                     text, c->hash_off.p, d_info, d_hashes);
   }));
   return sync_ctx(c);
 }

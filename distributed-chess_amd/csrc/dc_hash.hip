@@ -130,6 +130,7 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
                                                                   const char* __restrict__ hist, u32 hist_len,
                                                                   u32 hist_tokens, const char* __restrict__ names,
                                                                   const u32* __restrict__ names_off,
+                                                                  const uint8_t* __restrict__ info,
                                                                   uint8_t* __restrict__ out) {
   // templates and the lanes' move tokens in one LDS pool (a piece in LDS is an
   // offset into it; names and the start history are global pointers)
@@ -144,8 +145,14 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   const u32 g = blockIdx.x * kHashThreads + tid;
   const bool active = g < n_games;
   // ---- pass 1: the final turn
+  // info != nullptr (round 5): the replay kernel ran first (k_replay_ref4's
+  // INFO form, dc_replay_info's per-ply byte: the mover's kind | 8 on a
+  // capture, 0xFF for a rejected move), so the turn is the accepted plies'
+  // parity and pass 2 reads kind and capture from it; no ply is validated here
   u32 stm = stm0;
-  if (active) {
+  if (active && info) {
+    for (u32 p = 0; p < n_plies; ++p) stm ^= (u32)(info[(size_t)p * n_games + g] != 0xFFu);
+  } else if (active) {
     Board b = start;
     u32 bits = 0;
     for (u32 p = 0; p < n_plies; ++p) {
@@ -216,12 +223,19 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           rem = 0;
           while (ply < n_plies && rem == 0) {
             const u32 p = ply++;
-            if (p < kAccPlies && ((accb[p >> 5][tid] >> (p & 31)) & 1) == 0) continue;  // rejected in pass 1
+            u32 code = 0;
+            if (info) {  // kernel-uniform
+              code = info[(size_t)p * n_games + g];
+              if (code == 0xFFu) continue;  // rejected
+            } else if (p < kAccPlies && ((accb[p >> 5][tid] >> (p & 31)) & 1) == 0) {
+              continue;  // rejected in pass 1
+            }
             const u32 m = moves[(size_t)p * n_games + g];
-            if (p >= kAccPlies && (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK)) continue;
+            if (!info && p >= kAccPlies && (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK)) continue;
             const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
-            const u32 ki = kind_index(nibble(b, f) >> 1);
-            const bool cap = (occupied(b) >> t) & 1;
+            // info's kinds are P0 N1 B2 R3 Q4 K5 (kind_index's order; an unknown kind never moves)
+            const u32 ki = info ? (code & 7u) : kind_index(nibble(b, f) >> 1);
+            const bool cap = info ? (code & 8u) != 0 : ((occupied(b) >> t) & 1) != 0;
             u32 n = 0;
             if (ntok) mytok[n++] = ' ';
             // N's decimal digits written last-first straight into the token
@@ -436,10 +450,10 @@ hipError_t launch_escape_write(hipStream_t st, const char* names, const u32* off
 
 hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                                  u32 n_plies, const char* hist, u32 hist_len, u32 hist_tokens, const char* names,
-                                 const u32* names_off, uint8_t* out) {
+                                 const u32* names_off, const uint8_t* info, uint8_t* out) {
   if (n_games == 0) return hipSuccess;
   hipLaunchKernelGGL(k_state_hash_ref, dim3(blocks_for(n_games, kHashThreads)), dim3(kHashThreads), 0, st, start, stm0,
-                     moves, n_games, n_plies, hist, hist_len, hist_tokens, names, names_off, out);
+                     moves, n_games, n_plies, hist, hist_len, hist_tokens, names, names_off, info, out);
   return hipGetLastError();
 }
 
