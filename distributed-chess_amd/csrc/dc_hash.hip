@@ -20,11 +20,14 @@
 // k_escape_write, below) from raw UTF-8 resident in HBM; the tokens the kernel
 // appends are plain ASCII.
 //
-// Per lane: pass 1 replays the game (ref_verdict + make per ply) to learn the
-// final turn (the first JSON field) and records each ply's verdict as one bit
-// in LDS (the first kAccPlies plies); pass 2 streams the JSON bytes into the
-// sponge, re-making only the accepted moves from those bits (plies past
-// kAccPlies are validated again).  Round 1 validated every ply twice.
+// Per lane: pass 1 learns the final turn (the first JSON field); pass 2
+// streams the JSON bytes into the sponge, making only the accepted moves.
+// Since round 5 the host runs the replay kernel's per-ply info pass first
+// (info: verdict, mover kind, capture per ply), so pass 1 is the accepted
+// plies' parity and pass 2 validates nothing.  Without info (a batch past
+// the replay kernel's one buffer descriptor), pass 1 replays the game
+// (ref_verdict + make per ply) and keeps each ply's verdict as one bit in LDS
+// (the first kAccPlies plies; later plies are validated again in pass 2).
 // Bytes are produced into the lane's 136-byte block in LDS by a small piece
 // state machine (template strings, names, start history, per-move tokens,
 // board cells); every lane emits exactly one block per step, so the
