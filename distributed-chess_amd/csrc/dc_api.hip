@@ -154,10 +154,11 @@ struct dc_ctx {
     // the capacities a captured graph was sized with (test knobs
     // DCHESS_PERFT_WIDE_MAX / _WIDE_LEVEL_MAX): a changed knob re-captures
     uint64_t wide_words, wide_level;
+    bool front;  // the sequence is k_front + k_count3c
     bool operator==(const PerftKey& o) const {
       return rules == o.rules && depth == o.depth && split == o.split && shard == o.shard &&
              n_shards == o.n_shards && stm == o.stm && k4 == o.k4 && n_root == o.n_root && epoch == o.epoch &&
-             wide_words == o.wide_words && wide_level == o.wide_level;
+             wide_words == o.wide_words && wide_level == o.wide_level && front == o.front;
     }
   } pkey{};
   hipGraphExec_t pgraph = nullptr;
@@ -172,6 +173,9 @@ struct dc_ctx {
   // the last perft_impl needed the exact (host-sized) rerun: its speculative
   // level capacities overflow, so dc_perft_repeat_device must not replay them
   bool last_exact = false;
+  // the last perft_impl ran the one-launch front end (k_front); false when it
+  // declined the position (the legacy chain ran) or was not eligible
+  bool last_front = false;
   const char* last_final = "count2";  // timing name of the last perft's final stage
   struct RootStage {
     Board b[dc::kMaxPerftRoots];
@@ -193,11 +197,16 @@ struct dc_ctx {
   std::string hist_text;   // the escaped start history (host side of the H2D copy)
   DBuf<uint8_t> hashes;
   DBuf<u64> bitmap, digests, stats5;
+  // the state hash's replay pre-pass is skipped past this many bytes of its
+  // buffers (unlimited; dc_test_hash_prepass_max lowers it to test the fallback)
+  u64 hash_prepass_max = ~0ull;
   DBuf<u32> move_words;  // k_count3c: the final stage's parents as move words below their grandparents
   DBuf<u64> move_words64;  // ... as 64-bit words (REF perft(8): more than 2^20 grandparents)
   DBuf<dc::Range> slice_rng;  // the sliced final stage (REF perft(9)): one slice's node and word Ranges
   DBuf<u32> slice_ctr;        // ... and its group counter
   DBuf<u32> top_words;   // k_expand_top's last ply as move words (k_make_count makes it)
+  DBuf<uint8_t> front_st;  // k_front's look-back slots, a dc::FrontState (zeroed once; k_count3c re-zeroes them)
+  uint8_t* front_st_zeroed = nullptr;
   // transaction-signature check: staged strings / offsets / actions / turns,
   // and the G table (built on first use)
   DBuf<char> tx_text;
@@ -226,6 +235,7 @@ struct dc_ctx {
     rng.release();
     desc.release();
     top_words.release();
+    front_st.release();
     move_words.release();
     dfs_stack.release();
     move_words64.release();
@@ -680,15 +690,39 @@ extern "C" __attribute__((visibility("default"))) int dc_test_live_timeout(dc_ct
   return DC_SUCCESS;
 }
 
+// live_call's answer when a LiveHold is active: the caller takes the launched path.
+constexpr int kLiveDeclined = -1000;
+
+// Test hook (not in the header): 1 when the context's last perft ran the
+// one-launch front end (k_front), 0 when it took the legacy chain.
+extern "C" __attribute__((visibility("default"))) int dc_test_perft_last_front(const dc_ctx* c) {
+  return c ? (int)c->last_front : -1;
+}
+
+// Test hook (not in the header): the state hash's pre-pass budget in bytes, so
+// a test can force the hash kernel's own validation path and compare hashes.
+extern "C" __attribute__((visibility("default"))) int dc_test_hash_prepass_max(dc_ctx* c, uint64_t bytes) {
+  if (!c) return DC_EINVAL;
+  c->hash_prepass_max = bytes;
+  return DC_SUCCESS;
+}
+
 // One request through the mailbox.  pos_out (apply) may alias pos.
+// The whole call runs under g_live_mu (then c->live_mu), and whether a hold is
+// active is decided under that lock: a LiveHold counts itself before it takes
+// g_live_mu, so either this call sees it and declines, or the hold's
+// constructor runs after this call and stops the wave it may have started.
+// (Round 5 read the hold count and live_running before any lock: a hold that
+// stopped the waves in between could be followed by a fresh wave, and the
+// hold's hipFree then waited for that wave's lease.)
 static int live_call(dc_ctx* c, bool apply, bool fide, const dc_pos* pos, const uint16_t* moves, uint32_t n,
                      uint8_t* verdicts, uint8_t* info, dc_pos* pos_out) {
+  std::lock_guard<std::mutex> g(g_live_mu);
+  if (g_live_hold.load() != 0) return kLiveDeclined;
   // About to start a wave: the process keeps one resident at a time, since
   // two contexts' live streams may share a hardware queue, where the second
   // wave would wait behind the first for its whole lease.
-  std::unique_lock<std::mutex> g(g_live_mu, std::defer_lock);
   if (!c->live_running) {
-    g.lock();
     for (dc_ctx* o : g_live_ctxs)
       if (o != c) {
         std::lock_guard<std::mutex> l(o->live_mu);
@@ -762,6 +796,7 @@ static int live_call(dc_ctx* c, bool apply, bool fide, const dc_pos* pos, const 
   return DC_SUCCESS;
 }
 
+// (the hold count read here is only a hint; live_call decides under g_live_mu)
 static bool live_eligible(const dc_ctx* c, uint32_t n) {
   return c->live_lease_us && n <= dc::kLiveMax && !c->profiling && g_live_hold.load() == 0;
 }
@@ -772,7 +807,10 @@ int dc_validate_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, const uint16
   ENTER(c);
   if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
   if (n == 0) return DC_SUCCESS;
-  if (live_eligible(c, n)) return live_call(c, false, rules == DC_RULES_FIDE, pos, moves, n, verdicts, nullptr, nullptr);
+  if (live_eligible(c, n)) {
+    const int e = live_call(c, false, rules == DC_RULES_FIDE, pos, moves, n, verdicts, nullptr, nullptr);
+    if (e != kLiveDeclined) return e;
+  }
   LiveHold live_hold_;  // the launched path (ENTER_WORK)
   if (n <= kHostIoBatch) {  // pinned, read in place by the kernel
     if (!c->host_io) {
@@ -813,7 +851,10 @@ int dc_apply_batch(dc_ctx* c, uint32_t rules, dc_pos* pos, const uint16_t* moves
   ENTER(c);
   if (rules > DC_RULES_FIDE || (n && (!pos || !moves || !verdicts))) return DC_EINVAL;
   if (n == 0) return DC_SUCCESS;
-  if (live_eligible(c, n)) return live_call(c, true, rules == DC_RULES_FIDE, pos, moves, n, verdicts, info, pos);
+  if (live_eligible(c, n)) {
+    const int e = live_call(c, true, rules == DC_RULES_FIDE, pos, moves, n, verdicts, info, pos);
+    if (e != kLiveDeclined) return e;
+  }
   LiveHold live_hold_;  // the launched path (ENTER_WORK)
   if (n <= kHostIoBatch) {  // pinned, read and written in place by the kernel
     if (!c->host_io) {
@@ -1084,9 +1125,18 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
 #ifndef DC_HASH_PRE
 #define DC_HASH_PRE 1  // (0: the round-4 single kernel, for A/B only)
 #endif
-  if (DC_HASH_PRE && n_plies > 0 && (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull) {
-    HIP_TRY(c->replay_info.ensure((size_t)n_games * n_plies));
-    HIP_TRY(c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(n_games)));
+  // The pre-pass is an optimisation: when its buffers (up to ~2 GiB near the
+  // move bound) cannot be had, or exceed the context's pre-pass budget (a test
+  // hook), the hash kernel validates on its own instead of the call failing.
+  const u64 pre_bytes = (u64)n_games * n_plies + 8 * (5 + 5 * (u64)dc::replay_partials(n_games));
+  bool pre = DC_HASH_PRE && n_plies > 0 && (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull &&
+             pre_bytes <= c->hash_prepass_max;
+  if (pre && (c->replay_info.ensure((size_t)n_games * n_plies) != hipSuccess ||
+              c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(n_games)) != hipSuccess)) {
+    (void)hipGetLastError();
+    pre = false;
+  }
+  if (pre) {
     bool host_written = false;
     HIP_TRY(c->timed("state_hash_replay", (u64)n_games * n_plies, [&] {
       return dc::launch_replay_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, nullptr, nullptr, c->stats5.p,
@@ -1368,9 +1418,11 @@ int write_root_host(dc_ctx* c, const dc_pos* pos, u32 n = 1) {
 }
 
 // the staged roots to the device root arrays (stream-ordered)
-int upload_roots(dc_ctx* c, u32 n) {
+int upload_roots(dc_ctx* c, u32 n, bool meta = true) {
   HIP_TRY(hipMemcpyAsync(c->root.p, c->root_host->b, n * sizeof(Board), hipMemcpyHostToDevice, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->root_meta.p, c->root_host->meta, n * sizeof(uint16_t), hipMemcpyHostToDevice, c->stream));
+  if (meta)  // (REF reads no castle / ep: one graph node less per run)
+    HIP_TRY(hipMemcpyAsync(c->root_meta.p, c->root_host->meta, n * sizeof(uint16_t), hipMemcpyHostToDevice,
+                           c->stream));
   return DC_SUCCESS;
 }
 
@@ -1397,9 +1449,71 @@ static bool fide_top_short() {
 // copy.  *host_sync is set when a level size had to be read back on the host
 // (exact mode or a level beyond the speculative budget): such a sequence
 // depends on data and is never captured as a graph.
+// DC_FRONT=0 (A/B build): REF perft(6) / perft(7) take the round-5 chain.
+static bool front_enabled() {
+  static const bool on = [] {
+    const char* e = dc::ab_env("DC_FRONT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+// REF perft(6) / perft(7) of one root, unsharded or a strided shard of ply 3:
+// the one-launch front end (k_front) + k_count3c.
+static bool front_eligible(uint32_t rules, uint32_t depth, uint32_t split_depth, uint32_t n_shards, u32 n_pos) {
+  if (rules != DC_RULES_REF || n_pos != 1 || (depth != 6 && depth != 7) || !front_enabled() || !fused3_enabled())
+    return false;
+  const u32 S = std::max<u32>(1, std::min(split_depth, depth - 2));
+  return n_shards == 1 || (S == 3 && !shard_contiguous());
+}
+
+// k_front's sequence: the root upload (stage_root), k_front, k_count3c.
+static int front_enqueue(dc_ctx* c, const dc_pos* pos, uint32_t depth, uint32_t shard, uint32_t n_shards,
+                         bool stage_root) {
+  if (!c->res_host) HIP_TRY(hipHostMalloc((void**)&c->res_host, sizeof(dc::PerftResult)));
+  if (!c->root_host) {
+    HIP_TRY(hipHostMalloc((void**)&c->root_host, sizeof(*c->root_host)));
+    c->root_host->n = 0;
+  }
+  HIP_TRY(c->res.ensure(1));
+  HIP_TRY(c->rng.ensure(16));
+  HIP_TRY(c->root.ensure(dc::kMaxPerftRoots));
+  HIP_TRY(c->root_meta.ensure(dc::kMaxPerftRoots));
+  HIP_TRY(c->front_st.ensure(sizeof(dc::FrontState)));
+  dc::FrontState* fst = reinterpret_cast<dc::FrontState*>(c->front_st.p);
+  if (c->front_st_zeroed != c->front_st.p) {  // a new state block (stream-ordered before its first use)
+    HIP_TRY(hipMemsetAsync(c->front_st.p, 0, sizeof(dc::FrontState), c->stream));
+    c->front_st_zeroed = c->front_st.p;
+  }
+  // the grandparents' index is a move word's upper 20 bits
+  const u32 cap_b = (u32)dc::kMoveWordNodesMax;
+  const u64 cap_w = std::min<u64>((u64)cap_b * kBranchBound, 0xFFFFFFFFull);
+  int e = ensure_level(c, 0, cap_b, false);
+  if (e != DC_SUCCESS) return e;
+  HIP_TRY(c->move_words.ensure(cap_w));
+  if (stage_root) {
+    e = write_root_host(c, pos, 1);
+    if (e == DC_SUCCESS) e = upload_roots(c, 1, false);
+    if (e != DC_SUCCESS) return e;
+  }
+  dc::Range* rng = c->rng.p + 8;  // [8] the grandparents, [9] the move words
+  HIP_TRY(c->timed("front", 0, [&] {
+    return dc::launch_front(c->stream, pos->stm, depth, c->root.p, shard, n_shards, c->nodes[0].p, c->tags[0].p,
+                            cap_b, c->move_words.p, cap_w, c->res.p, rng, fst);
+  }));
+  c->last_final = "count2";
+  const int stm_g = pos->stm ^ (int)((depth - 3) & 1);  // the grandparents are ply depth - 3
+  HIP_TRY(c->timed("count2", 0, [&] {
+    return dc::launch_count3c(c->stream, stm_g, c->nodes[0].p, c->tags[0].p, rng, rng + 1, c->move_words.p,
+                              c->res.p, nullptr, fst);
+  }));
+  return DC_SUCCESS;
+}
+
 int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
                   uint32_t shard, uint32_t n_shards, bool exact, bool* host_sync, bool stage_root = true,
-                  u32 n_pos = 1) {
+                  u32 n_pos = 1, bool front = false) {
+  if (front && !exact) return front_enqueue(c, pos, depth, shard, n_shards, stage_root);
   const bool fide = rules == DC_RULES_FIDE;
   const bool sharded = n_shards > 1;
   u32 F = depth >= 3 ? depth - 2 : 1;             // level handed to the final stage
@@ -1457,7 +1571,7 @@ int perft_enqueue(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, 
   // root upload from pinned memory (stage_root = false: the caller staged it)
   if (stage_root) {
     e = write_root_host(c, pos, n_pos);
-    if (e == DC_SUCCESS) e = upload_roots(c, n_pos);
+    if (e == DC_SUCCESS) e = upload_roots(c, n_pos, fide);
     if (e != DC_SUCCESS) return e;
   }
   // REF final stage over the last three plies (k_count3c): the level F is
@@ -1707,10 +1821,11 @@ static bool perft_graphs_enabled() {
 // which removes the per-kernel launch gaps.  The root position
 // is read from the pinned staging block when the graph runs.
 int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth, uint32_t shard,
-              uint32_t n_shards, bool exact, dc::PerftResult* out, u32 n_pos = 1) {
+              uint32_t n_shards, bool exact, dc::PerftResult* out, u32 n_pos = 1, bool front = false) {
   const bool graphable = !exact && !c->profiling && perft_graphs_enabled();
-  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(), n_pos,
-                       g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
+  front = front && !exact;
+  dc_ctx::PerftKey key{rules,  depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(), n_pos,
+                       g_alloc_epoch.load(), wide_words_max(), wide_level_bytes(), front};
   if (graphable && c->pgraph && c->pkey == key) {
     int e = write_root_host(c, pos, n_pos);
     if (e != DC_SUCCESS) return e;
@@ -1721,7 +1836,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
     return DC_SUCCESS;
   }
   bool host_sync = false;
-  int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, exact, &host_sync, true, n_pos);
+  int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, exact, &host_sync, true, n_pos, front);
   if (e != DC_SUCCESS) return e;
   HIP_TRY(hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream));
   e = sync_ctx(c);
@@ -1739,7 +1854,7 @@ int perft_run(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uint
     return DC_SUCCESS;
   }
   bool hs = false;
-  int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, true, n_pos);
+  int ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, true, n_pos, front);
   if (ce == DC_SUCCESS &&
       hipMemcpyAsync(c->res_host, c->res.p, sizeof(dc::PerftResult), hipMemcpyDeviceToHost, c->stream) != hipSuccess)
     ce = DC_EHIP;
@@ -1768,7 +1883,16 @@ int perft_impl(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t depth, uin
     return DC_SUCCESS;
   }
   dc::PerftResult r;
-  int e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r, n_pos);
+  // the one-launch front end where eligible; a position it declines (a top
+  // past its LDS bounds, a level past its capacity) takes the legacy chain,
+  // and speculative capacities that overflow there the exact rerun
+  bool front = front_eligible(rules, depth, split_depth, n_shards, n_pos);
+  int e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r, n_pos, front);
+  if (e == DC_SUCCESS && front && r.overflow && r.front_declined) {
+    front = false;
+    e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, false, &r, n_pos, false);
+  }
+  c->last_front = front;
   c->last_exact = e == DC_SUCCESS && r.overflow;
   if (c->last_exact) e = perft_run(c, rules, pos, depth, split_depth, shard, n_shards, true, &r, n_pos);
   if (e != DC_SUCCESS) return e;
@@ -1821,8 +1945,10 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
                        u32 n_pos = 1) {
   if (n_runs == 0) return DC_SUCCESS;
   HIP_TRY(c->rcur.ensure(1));  // before the key: an allocation moves the epoch
-  dc_ctx::PerftKey key{rules, depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(), n_pos,
-                       g_alloc_epoch.load(), wide_words_max(), wide_level_bytes()};
+  // (a graph captured after a declined front holds the legacy chain: front false)
+  dc_ctx::PerftKey key{rules,  depth, split_depth, shard, n_shards, (u32)pos->stm, (u32)perft_k4_forced(), n_pos,
+                       g_alloc_epoch.load(), wide_words_max(), wide_level_bytes(),
+                       front_eligible(rules, depth, split_depth, n_shards, n_pos)};
   const bool graphable = !c->profiling && perft_graphs_enabled();
   // capture `runs` runs of the sequence back to back (the result copy is part
   // of the graph: its destination is the cursor)
@@ -1831,7 +1957,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
     bool hs = false;
     int ce = DC_SUCCESS;
     for (u32 r = 0; r < runs && ce == DC_SUCCESS && !hs; ++r) {
-      ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false, n_pos);
+      ce = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &hs, false, n_pos, key.front);
       if (ce == DC_SUCCESS && dc::launch_copy_result(c->stream, c->res.p, c->rcur.p) != hipSuccess) ce = DC_EHIP;
     }
     hipGraph_t g = nullptr;
@@ -1862,6 +1988,7 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
       return DC_SUCCESS;
     }
     key.epoch = g_alloc_epoch.load();
+    key.front = c->last_front;
     if (graphable) {
       for (hipGraphExec_t* ge : {&c->rgraph, &c->rgraph_batch}) {
         if (*ge) (void)hipGraphExecDestroy(*ge);
@@ -1900,7 +2027,8 @@ static int repeat_runs(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t de
       HIP_TRY(hipGraphLaunch(c->rgraph, c->stream));  // perft + result copy
     } else {
       bool host_sync = false;
-      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync, true, n_pos);
+      int e = perft_enqueue(c, rules, pos, depth, split_depth, shard, n_shards, false, &host_sync, true, n_pos,
+                            key.front);
       if (e != DC_SUCCESS) return e;
       HIP_TRY(dc::launch_copy_result(c->stream, c->res.p, c->rcur.p));
     }
@@ -1947,7 +2075,11 @@ int dc_perft_batch(dc_ctx* c, uint32_t rules, const dc_pos* pos, uint32_t n_pos,
   e = perft_impl(c, rules, pos, depth, 1, 0, 1, div, root_moves, &nr, &total, n_pos, parent);
   if (e != DC_SUCCESS) return e;
   for (u32 i = 0; i < n_pos; ++i) totals[i] = 0;
-  for (u32 k = 0; k < nr; ++k) totals[parent[k] < n_pos ? parent[k] : 0] += div[k];
+  // a root move tagged with a position outside the batch can only come from a
+  // device fault: an error, never a count folded into some position's total
+  for (u32 k = 0; k < nr; ++k)
+    if (parent[k] >= n_pos) return DC_EHIP;
+  for (u32 k = 0; k < nr; ++k) totals[parent[k]] += div[k];
   if (divide) std::copy(div, div + nr, divide);
   if (root_pos) std::copy(parent, parent + nr, root_pos);
   if (n_root) *n_root = nr;

@@ -244,22 +244,34 @@ __device__ __forceinline__ Analysis analyse(const FPos<STM>& f, bool with_danger
   // neither a slider check nor a pin: a wave none of whose lanes has one
   // skips that line's two scans (round 4: the eight scans were ~19 % of the
   // FIDE final stage, tools/bbprof_inline.py)
-  if (__ballot((l.file & f.tO) != 0)) {
+  // Round 6: the four gates' operands are made together before the first gate
+  // (opaque), and each stays live past its own branch (an empty asm reading
+  // it after the if), so no VALU write can land on a gate compare's source
+  // registers between the compare and its VCCZ branch -- the shape
+  // tools/vccz_check.py --any flagged in 16 FIDE kernels after round 5 (there
+  // the next gate's v_and_b32 overwrote them).
+  u64 g_file = l.file & f.tO, g_rank = l.rank & f.tO, g_diag = l.diag & f.tD, g_anti = l.anti & f.tD;
+  asm volatile("" : "+v"(g_file), "+v"(g_rank), "+v"(g_diag), "+v"(g_anti));
+  if (__ballot(g_file != 0)) {
     scan_dir<STM, 0>(f, kup, kdn, l, chk, pin);
     scan_dir<STM, 1>(f, kup, kdn, l, chk, pin);
   }
-  if (__ballot((l.rank & f.tO) != 0)) {
+  asm volatile("" ::"v"(g_file));
+  if (__ballot(g_rank != 0)) {
     scan_dir<STM, 2>(f, kup, kdn, l, chk, pin);
     scan_dir<STM, 3>(f, kup, kdn, l, chk, pin);
   }
-  if (__ballot((l.diag & f.tD) != 0)) {
+  asm volatile("" ::"v"(g_rank));
+  if (__ballot(g_diag != 0)) {
     scan_dir<STM, 4>(f, kup, kdn, l, chk, pin);
     scan_dir<STM, 5>(f, kup, kdn, l, chk, pin);
   }
-  if (__ballot((l.anti & f.tD) != 0)) {
+  asm volatile("" ::"v"(g_diag));
+  if (__ballot(g_anti != 0)) {
     scan_dir<STM, 6>(f, kup, kdn, l, chk, pin);
     scan_dir<STM, 7>(f, kup, kdn, l, chk, pin);
   }
+  asm volatile("" ::"v"(g_anti));
 #else
   scan_dir<STM, 0>(f, kup, kdn, l, chk, pin);
   scan_dir<STM, 1>(f, kup, kdn, l, chk, pin);

@@ -19,7 +19,7 @@ struct PerftResult {
   u32 next_chunk;  // k_count2c's dynamic chunk counter (zeroed with the block)
   u64 level_n[16];
   u32 dfs_next;    // k_perft_dfs's frontier cursor (zeroed with the block)
-  u32 pad0;
+  u32 front_declined;  // k_front: the top or a level did not fit it (overflow is set too): rerun without it
   uint8_t root_parent[256];  // which root position each root move belongs to (a batch: dc_perft_batch)
 };
 
@@ -106,8 +106,12 @@ hipError_t launch_final(hipStream_t st, u32 rules, int stm, int plies, const Boa
 constexpr u64 kMoveWordNodesMax = 1ull << 20;
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
                               const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap);
+struct FrontState;
+// fst != nullptr (after launch_front): the front end's look-back slots are
+// cleared for the next run.
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter = nullptr);
+                          const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter = nullptr,
+                          FrontState* fst = nullptr);
 // The same with u64 words {grandparent index << 12 | f | t << 6} (no 2^20
 // grandparent limit): REF perft(8)'s final stage below ply 5.
 hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const Range* rng, u64 n_bound,
@@ -120,6 +124,27 @@ hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const u
 // than cap words sets res->overflow.
 hipError_t launch_wide_slice(hipStream_t st, const Range* lvl, const u64* chunk_base, const Range* words_total,
                              u64 s0, u64 len, Range* out, u32* counter, PerftResult* res, u64 cap);
+
+// REF perft(6) / perft(7) front end in one launch (k_front, round 6): the root
+// (device) -> the final stage's grandparents (ply 3 at depth 6, ply 4 at depth 7)
+// as boards + tags in out (capacity cap_b <= 2^20) and their children as u32
+// move words in mw (capacity cap_w), rng_out[0] / rng_out[1] their Ranges;
+// then launch_count3c(stm_g = side to move at the grandparents, rng_out,
+// rng_out + 1, fst).  Unsharded, or this rank's strided shard of ply 3.  The
+// state block (the items' look-back slots) must be zero before the first
+// launch; the launch_count3c given it clears them again.  A top past the
+// kernel's LDS bounds (more than 128 root moves or 2,048 ply-2 nodes), an item
+// of more than 1,024 boards or a level past its capacity sets overflow and
+// front_declined.
+constexpr u32 kFrontItemsMax = 1u << 16;
+struct FrontState {
+  u32 n_items, pad;
+  u64 agg[kFrontItemsMax];
+  u64 incl[kFrontItemsMax];
+};
+hipError_t launch_front(hipStream_t st, int stm0, u32 depth, const Board* root, u32 shard, u32 n_shards, Board* out,
+                        uint16_t* out_tags, u32 cap_b, u32* mw, u64 cap_w, PerftResult* res, Range* rng_out,
+                        FrontState* fst);
 
 // K4 (REF): per-lane DFS over L plies below the frontier level `rng` (1 <= L <= 3),
 // each level-L node bulk-counted over the last two plies (perft depth = frontier

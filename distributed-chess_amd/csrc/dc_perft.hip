@@ -747,6 +747,414 @@ __global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ n
   }
 }
 
+// ------------------------------------------------- k_front (REF, round 6)
+// The whole front end of REF perft(6) / perft(7) in one launch: root -> the
+// final stage's grandparents (ply 3 + E) as boards and their children as u32
+// move words for k_count3c, replacing k_expand_top (one workgroup), k_make_count,
+// k_chunk_scan, k_level_write, k_chunk_scan and k_level_moves (~67 us of
+// dependent, latency-bound launches per run, round 5).
+//
+//  * Every block rebuilds plies 1 and 2 and the ply-3 move counts of the ply-2
+//    nodes in LDS (a few hundred nodes: cheaper than a launch and a global
+//    round trip), so every block knows the canonical ply-3 order -- ply-1
+//    parents in order, ref_for_each_move's class-major order within a parent
+//    -- that the strided shards of dc_perft_shard are cut from.
+//  * Items of P3 consecutive ply-3 nodes of this rank's shard (P3 sized so one
+//    pass of the resident grid covers the shard) are expanded E plies (0:
+//    perft(6), 1: perft(7)); the boards and their move words are counted
+//    first, and the item's offsets come from a decoupled look-back over the
+//    earlier items' published (boards, words) -- no same-address atomics (a
+//    first version took both from two global cursors: 768 blocks queued on
+//    them for up to ~15 us, tools/front_trace.py) -- so both levels come out
+//    in the canonical order of the legacy chain.
+//  * Every serial walk is split over the four class groups of
+//    ref_group_moves, one wave per group (a lane walks a quarter of a
+//    position's moves): one lane walking ~25 moves was ~7 us of the first
+//    version's ~30 us per item.
+//  * The block holding the last item publishes the two Ranges (or, when a
+//    level is past its capacity or the top past the LDS bounds, flags
+//    overflow + front_declined: the host reruns on the legacy chain).  Block
+//    0 clears the run's result block and records the root moves.
+constexpr u32 kFrontPly1Max = 128;    // root moves (more: the legacy chain)
+constexpr u32 kFrontPly2Max = 2048;   // ply-2 nodes (more: the legacy chain)
+constexpr u32 kFrontP3Max = 64;       // ply-3 nodes per item
+constexpr u32 kFrontBoardsMax = 1024; // boards per item (more: declined)
+constexpr u32 kFrontSlotW = 2048;     // move-word slots of one window
+
+#ifdef DC_AB_KNOBS
+// A/B build: k_front's timeline (wall clock, 100 MHz) for the first
+// kFrontTraceBlocks blocks: kFrontTraceWords stamps each, read back by
+// dc_ab_front_trace (tools/front_trace.py).
+constexpr u32 kFrontTraceBlocks = 64, kFrontTraceWords = 16;
+__device__ u64 g_front_trace[kFrontTraceBlocks * kFrontTraceWords];
+#define DC_FRONT_STAMP(k)                                                                     \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.x < kFrontTraceBlocks)                                   \
+      g_front_trace[blockIdx.x * kFrontTraceWords + (k)] = wall_clock64();                    \
+  } while (0)
+#else
+#define DC_FRONT_STAMP(k) \
+  do {                    \
+  } while (0)
+#endif
+
+struct FrontShared {
+  Board p1[kFrontPly1Max];
+  u32 w2[kFrontPly2Max];     // ply-2 nodes: ply-1 index << 12 | f | t << 6
+  u32 off3[kFrontPly2Max];   // their ply-3 move counts, then exclusive offsets
+  Board b2[kFrontP3Max];     // an item's ply-3 nodes' parents
+  Board b3[kFrontP3Max];     // an item's ply-3 nodes
+  u32 r3[kFrontP3Max];       // ... their rank among the parent's moves
+  uint16_t t3[kFrontP3Max];  // ... their tags (root move index)
+  uint16_t m1[kFrontPly1Max];
+  u32 gc[4][kFrontPly1Max];  // per-group move counts (ply 2, selection, ply 4)
+  u32 noff[kFrontPly1Max];   // per-node move offsets (ply 2, ply 4)
+  u32 slot4[kFrontBoardsMax];            // E = 1: an item's ply-4 moves (ply-3 node << 12 | f | t << 6)
+  uint16_t gw[4][kFrontBoardsMax];       // per-(group, board) word counts
+  u32 woff[kFrontBoardsMax];             // per-board word offsets
+  u32 slotw[kFrontSlotW];                // move words of one window
+  u64 red[4][3];
+  u64 look[3];
+  u32 g1[4];
+  u32 wsum[4];
+  u32 n4, bad, jm;
+};
+
+// Per item: the published aggregate and inclusive prefix (FrontState, dc_perft.h),
+// each one u64 {ready:1 | bad:1 | boards:22 | words:40}.  The slots are zero
+// when a run starts: the k_count3c after each k_front zeroes the run's n_items.
+__device__ __forceinline__ u64 front_pack(u64 bad, u64 nb, u64 nw) {
+  bad |= (nb >> 22) | (nw >> 40) ? 1ull : 0ull;  // (a prefix past the fields is flagged, never wrapped)
+  return (1ull << 63) | (bad << 62) | ((nb & 0x3FFFFFull) << 40) | (nw & 0xFFFFFFFFFFull);
+}
+
+template <int S, class V>
+__device__ __forceinline__ void front_group_moves(u32 g, const Board& b, V&& visit) {
+  switch (g) {  // wave-uniform (g = wave index)
+    case 0: ref_group_moves<S, 0>(b, visit); break;
+    case 1: ref_group_moves<S, 1>(b, visit); break;
+    case 2: ref_group_moves<S, 2>(b, visit); break;
+    default: ref_group_moves<S, 3>(b, visit); break;
+  }
+}
+template <int S>
+__device__ __forceinline__ u32 front_group_count(u32 g, const Board& b) {
+  switch (g) {
+    case 0: return ref_group_count<S, 0>(b);
+    case 1: return ref_group_count<S, 1>(b);
+    case 2: return ref_group_count<S, 2>(b);
+    default: return ref_group_count<S, 3>(b);
+  }
+}
+
+// Sum of the (bad, boards, words) of every thread of the block.
+__device__ __forceinline__ void front_block_sum(FrontShared& sh, u64& bad, u64& nb, u64& nw) {
+  bad = wave_sum64(bad);
+  nb = wave_sum64(nb);
+  nw = wave_sum64(nw);
+  const u32 w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+    sh.red[w][0] = bad;
+    sh.red[w][1] = nb;
+    sh.red[w][2] = nw;
+  }
+  __syncthreads();
+  bad = sh.red[0][0] + sh.red[1][0] + sh.red[2][0] + sh.red[3][0];
+  nb = sh.red[0][1] + sh.red[1][1] + sh.red[2][1] + sh.red[3][1];
+  nw = sh.red[0][2] + sh.red[1][2] + sh.red[2][2] + sh.red[3][2];
+  __syncthreads();
+}
+
+// Decoupled look-back: the (bad, boards, words) of items [0, it), read
+// backwards in windows of 256 items; a window holding an inclusive prefix
+// ends the walk.  Every earlier item is held by a resident block that takes
+// its items in increasing order, so every slot waited on is written.  The
+// slots carry all the data exchanged, so the loads and stores are relaxed
+// device-scope atomics: acquire / release forms add a cache invalidate or
+// write-back per access (a spinning first version spent ~30 us here).
+__device__ __forceinline__ void front_lookback(FrontShared& sh, FrontState* st, u32 it, u64& bad, u64& nb, u64& nw) {
+  const u32 t = threadIdx.x;
+  bad = nb = nw = 0;
+  u32 hi = it;
+  while (hi > 0) {  // block-uniform
+    const u32 lo = hi > 256 ? hi - 256 : 0u;
+    const u32 j = lo + t;
+    u64 a = 0, inc = 0;
+    if (j < hi) {
+      do {
+        a = __hip_atomic_load(&st->agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } while (!(a >> 63));
+      inc = __hip_atomic_load(&st->incl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const bool has_inc = j < hi && (inc >> 63);
+    if (t == 0) sh.jm = 0;
+    __syncthreads();
+    if (has_inc) atomicMax(&sh.jm, j + 1);  // the last inclusive prefix of the window (+1)
+    __syncthreads();
+    const u32 jm = sh.jm;  // 0: none in this window
+    u64 v = 0;
+    if (jm && j == jm - 1) v = inc;
+    else if (j < hi && (!jm || j >= jm)) v = a;
+    u64 b1 = (v >> 62) & 1, n1 = (v >> 40) & 0x3FFFFFull, w1 = v & 0xFFFFFFFFFFull;
+    front_block_sum(sh, b1, n1, w1);
+    bad |= b1 ? 1ull : 0ull;
+    nb += n1;
+    nw += w1;
+    if (jm) break;
+    hi = lo;
+  }
+}
+
+// S0 = side to move at the root; E = plies between ply 3 and the boards written
+// (0: perft(6), boards = ply 3; 1: perft(7), boards = ply 4).  rng_out[0] = the
+// boards' Range, rng_out[1] = the words' (k_count3c's rng / rng_ch).
+template <int S0, int E>
+__global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p, u32 shard, u32 n_shards,
+                                               Board* __restrict__ out, uint16_t* __restrict__ out_tags, u32 cap_b,
+                                               u32* __restrict__ mw, u64 cap_w, PerftResult* __restrict__ res,
+                                               Range* __restrict__ rng_out, FrontState* __restrict__ st) {
+  constexpr int S1 = S0 ^ 1;       // side to move at ply 1 (and ply 3)
+  constexpr int SF = E ? S0 : S1;  // side to move at the boards written
+  __shared__ FrontShared sh;
+  const u32 t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  DC_FRONT_STAMP(0);
+  if (blockIdx.x == 0) {
+    static_assert(sizeof(PerftResult) % 8 == 0, "PerftResult is cleared in u64 words");
+    for (u32 k = t; k < sizeof(PerftResult) / 8; k += 256) reinterpret_cast<u64*>(res)[k] = 0;
+  }
+  const Board root = root_p[0];
+  // ---- ply 1: wave g counts and walks class group g of the root
+  if (lane == 0) sh.g1[wave] = front_group_count<S0>(wave, root);
+  __syncthreads();
+  const u32 n1 = sh.g1[0] + sh.g1[1] + sh.g1[2] + sh.g1[3];
+  bool ok = n1 <= kFrontPly1Max;  // block-uniform from here on
+  if (ok && lane == 0) {
+    u32 j = 0;
+    for (u32 g = 0; g < wave; ++g) j += sh.g1[g];
+    front_group_moves<S0>(wave, root, [&](int f, int to) { sh.m1[j++] = (uint16_t)(f | (to << 6)); });
+  }
+  __syncthreads();
+  if (ok && t < n1) {
+    const u32 m = sh.m1[t];
+    Board b = root;
+    ref_make(b, (int)(m & 63), (int)(m >> 6));
+    sh.p1[t] = b;
+    if (blockIdx.x == 0) res->root_moves[t] = (uint16_t)m;  // (after the clear: barriers between)
+  }
+  __syncthreads();
+  DC_FRONT_STAMP(1);
+  // ---- ply 2: wave w takes class group w of nodes lane and 64 + lane
+  u32 n2 = 0;
+  if (ok) {
+    for (u32 node = lane; node < kFrontPly1Max; node += 64)
+      sh.gc[wave][node] = node < n1 ? front_group_count<S1>(wave, sh.p1[node]) : 0u;
+    __syncthreads();
+    const u32 tot = t < kFrontPly1Max ? sh.gc[0][t] + sh.gc[1][t] + sh.gc[2][t] + sh.gc[3][t] : 0u;
+    const u32 ex = block_excl_scan32<4>(tot, sh.wsum, &n2);
+    if (t < kFrontPly1Max) sh.noff[t] = ex;
+    ok = n2 <= kFrontPly2Max;
+    __syncthreads();
+  }
+  DC_FRONT_STAMP(2);
+  if (ok) {
+    for (u32 node = lane; node < n1; node += 64) {
+      u32 j = sh.noff[node];
+      for (u32 g = 0; g < wave; ++g) j += sh.gc[g][node];
+      front_group_moves<S1>(wave, sh.p1[node], [&](int f, int to) { sh.w2[j++] = (node << 12) | (u32)f | ((u32)to << 6); });
+    }
+    __syncthreads();
+  }
+  DC_FRONT_STAMP(3);
+  // ---- ply-3 counts of the ply-2 nodes, scanned in place into offsets
+  u32 n3 = 0;
+  if (ok) {
+    for (u32 j = t; j < n2; j += 256) {
+      const u32 e = sh.w2[j];
+      Board b = sh.p1[e >> 12];
+      ref_make(b, (int)(e & 63), (int)((e >> 6) & 63));
+      sh.off3[j] = ref_count<S0>(b);
+    }
+    __syncthreads();
+    DC_FRONT_STAMP(4);
+    const u32 seg = (n2 + 255) / 256, a = min(n2, t * seg), z = min(n2, a + seg);
+    u32 s = 0;
+    for (u32 j = a; j < z; ++j) s += sh.off3[j];
+    u32 run = block_excl_scan32<4>(s, sh.wsum, &n3);
+    for (u32 j = a; j < z; ++j) {
+      const u32 v = sh.off3[j];
+      sh.off3[j] = run;
+      run += v;
+    }
+    __syncthreads();
+  }
+  DC_FRONT_STAMP(5);
+  if (blockIdx.x == 0 && t == 0) {
+    res->n_root = n1;
+    res->level_n[1] = n1;
+    res->level_n[2] = n2;
+    res->level_n[3] = n3;
+  }
+  // ---- this rank's ply-3 nodes (shard, shard + n_shards, ...) in items of P3
+  const u32 m3 = ok && n3 > shard ? (n3 - shard + n_shards - 1) / n_shards : 0u;
+  u32 P3 = max(1u, (m3 + gridDim.x - 1) / gridDim.x);
+  P3 = min(kFrontP3Max, max(P3, (m3 + kFrontItemsMax - 1) / kFrontItemsMax));
+  const u32 n_items = (m3 + P3 - 1) / P3;
+  if (blockIdx.x == 0 && t == 0) st->n_items = n_items;  // (k_count3c clears that many slots)
+  if (!ok || (n_items == 0 && blockIdx.x == 0)) {  // nothing to expand: block 0 publishes the result
+    if (blockIdx.x == 0 && t == 0) {
+      if (!ok) {
+        res->overflow = 1;
+        res->front_declined = 1;
+      }
+      rng_out[0] = Range{0, 0};
+      rng_out[1] = Range{0, 0};
+    }
+    return;
+  }
+  for (u32 it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const u32 k0 = it * P3, np3 = min(P3, m3 - k0);
+    // -- select the item's ply-3 nodes: parent by binary search (wave 0), the
+    //    rank's class group by one group count per wave, the move by one walk
+    if (wave == 0 && lane < np3) {
+      const u32 q = shard + (k0 + lane) * n_shards;
+      u32 lo = 0, hi = n2;  // the last ply-2 node whose offset is <= q (it has q's move)
+      while (hi - lo > 1) {
+        const u32 mid = (lo + hi) >> 1;
+        if (sh.off3[mid] <= q) lo = mid;
+        else hi = mid;
+      }
+      const u32 e = sh.w2[lo];
+      Board b2 = sh.p1[e >> 12];
+      ref_make(b2, (int)(e & 63), (int)((e >> 6) & 63));
+      sh.b2[lane] = b2;
+      sh.r3[lane] = q - sh.off3[lo];
+      sh.t3[lane] = (uint16_t)(e >> 12);
+    }
+    __syncthreads();
+    if (lane < np3) sh.gc[wave][lane] = front_group_count<S0>(wave, sh.b2[lane]);
+    __syncthreads();
+    if (lane < np3) {
+      u32 r = sh.r3[lane];
+      for (u32 g = 0; g < wave; ++g) r -= sh.gc[g][lane];  // (wraps when the move is in an earlier group)
+      if (r < sh.gc[wave][lane]) {
+        int f = 0, to = 0;
+        u32 k = 0;
+        const Board b2 = sh.b2[lane];
+        front_group_moves<S0>(wave, b2, [&](int ff, int tt) {
+          if (k == r) {
+            f = ff;
+            to = tt;
+          }
+          ++k;
+        });
+        Board b3 = b2;
+        ref_make(b3, f, to);
+        sh.b3[lane] = b3;
+      }
+    }
+    __syncthreads();
+    if (it == blockIdx.x) DC_FRONT_STAMP(6);
+    // -- the item's boards: E = 0 the ply-3 nodes, E = 1 their children
+    u32 nbd = np3;
+    bool bad = false;
+    if constexpr (E == 1) {
+      if (lane < np3) sh.gc[wave][lane] = front_group_count<S1>(wave, sh.b3[lane]);
+      __syncthreads();
+      const u32 tot = t < np3 ? sh.gc[0][t] + sh.gc[1][t] + sh.gc[2][t] + sh.gc[3][t] : 0u;
+      const u32 ex = block_excl_scan32<4>(tot, sh.wsum, &nbd);
+      if (t < 64) sh.noff[t] = ex;
+      __syncthreads();
+      bad = nbd > kFrontBoardsMax;  // block-uniform
+      if (!bad && lane < np3) {
+        u32 j = sh.noff[lane];
+        for (u32 g = 0; g < wave; ++g) j += sh.gc[g][lane];
+        front_group_moves<S1>(wave, sh.b3[lane],
+                              [&](int f, int to) { sh.slot4[j++] = (lane << 12) | (u32)f | ((u32)to << 6); });
+      }
+      __syncthreads();
+      if (it == blockIdx.x) DC_FRONT_STAMP(7);
+    }
+    if (bad) nbd = 0;
+    auto board_at = [&](u32 k) -> Board {
+      if constexpr (E == 1) {
+        const u32 e = sh.slot4[k];
+        Board b = sh.b3[e >> 12];
+        ref_make(b, (int)(e & 63), (int)((e >> 6) & 63));
+        return b;
+      } else {
+        return sh.b3[k];
+      }
+    };
+    // -- pass 1: per-(group, board) word counts, per-board offsets
+    for (u32 k = lane; k < nbd; k += 64) sh.gw[wave][k] = (uint16_t)front_group_count<SF>(wave, board_at(k));
+    __syncthreads();
+    const u32 seg = (nbd + 255) / 256, a = min(nbd, t * seg), z = min(nbd, a + seg);
+    u32 s = 0;
+    for (u32 k = a; k < z; ++k) s += (u32)sh.gw[0][k] + sh.gw[1][k] + sh.gw[2][k] + sh.gw[3][k];
+    u32 nw;
+    u32 run = block_excl_scan32<4>(s, sh.wsum, &nw);
+    for (u32 k = a; k < z; ++k) {
+      sh.woff[k] = run;
+      run += (u32)sh.gw[0][k] + sh.gw[1][k] + sh.gw[2][k] + sh.gw[3][k];
+    }
+    // -- publish, look back, publish the inclusive prefix
+    if (t == 0) {
+      __hip_atomic_store(&st->agg[it], front_pack(bad, nbd, nw), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    u64 pbad, pb, pw;
+    front_lookback(sh, st, it, pbad, pb, pw);  // (its barriers publish woff)
+    if (t == 0) {
+      __hip_atomic_store(&st->incl[it], front_pack(pbad | bad, pb + nbd, pw + nw), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (it == blockIdx.x) DC_FRONT_STAMP(8);
+    const u64 base_b = pb, base_w = pw;
+    const bool fits = !pbad && !bad && base_b + nbd <= cap_b;  // (else flagged below: no store)
+    // -- pass 2: the boards, then the words through LDS windows
+    if (fits)
+      for (u32 k = t; k < nbd; k += 256) {
+        store_board(out, base_b + k, board_at(k));
+        out_tags[base_b + k] = E == 1 ? sh.t3[sh.slot4[k] >> 12] : sh.t3[k];
+      }
+    for (u32 wb = 0; fits && wb < nw; wb += kFrontSlotW) {  // block-uniform
+      if (wb) __syncthreads();  // the previous window is stored
+      for (u32 k = lane; k < nbd; k += 64) {
+        u32 j = sh.woff[k];
+        for (u32 g = 0; g < wave; ++g) j += sh.gw[g][k];
+        const u32 c = sh.gw[wave][k];
+        if (c && j < wb + kFrontSlotW && j + c > wb) {
+          const u32 gidx = (u32)(base_b + k);
+          front_group_moves<SF>(wave, board_at(k), [&](int f, int to) {
+            if (j >= wb && j - wb < kFrontSlotW) sh.slotw[j - wb] = (gidx << 12) | (u32)f | ((u32)to << 6);
+            ++j;
+          });
+        }
+      }
+      __syncthreads();
+      const u32 ns = min(kFrontSlotW, nw - wb);
+      for (u32 r = t; r < ns; r += 256) {
+        const u64 o = base_w + wb + r;
+        if (o < cap_w) mw[o] = sh.slotw[r];
+      }
+    }
+    if (it == blockIdx.x) DC_FRONT_STAMP(9);
+    // -- the last item publishes the Ranges
+    if (it == n_items - 1 && t == 0) {
+      const u64 tb = base_b + nbd, tw = base_w + nw;
+      if (pbad || bad || tb > cap_b || tw > cap_w) {
+        res->overflow = 1;
+        res->front_declined = 1;
+        rng_out[0] = Range{0, 0};
+        rng_out[1] = Range{0, 0};
+      } else {
+        rng_out[0] = Range{0, tb};
+        rng_out[1] = Range{0, tw};
+      }
+    }
+    __syncthreads();  // the item's LDS is reused by the next item
+  }
+}
+
 // Children of the final level as 8-byte descriptors {parent index, move}.
 template <class R, int STM>
 __global__ __launch_bounds__(256) void k_emit_desc(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
@@ -1805,8 +2213,15 @@ template <int STM_G, u32 CAP, int MINW = 4, class W = u32>
 __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__ nodes, const uint16_t* __restrict__ tags,
                                                  const Range* __restrict__ rng, const Range* __restrict__ rng_ch,
                                                  const W* __restrict__ mw, u64* __restrict__ divide,
-                                                 u32* __restrict__ next_group) {
+                                                 u32* __restrict__ next_group, FrontState* __restrict__ fst) {
   __shared__ C2cShared<CAP> sh;
+  if (fst) {  // after k_front: its look-back slots are cleared for the next run
+    const u32 n = fst->n_items;
+    for (u32 k = blockIdx.x * 256 + threadIdx.x; k < n; k += gridDim.x * 256) {
+      fst->agg[k] = 0;
+      fst->incl[k] = 0;
+    }
+  }
   tag_hist_init(sh.hist);
   const u32 wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const bool t0 = wave == 0 && lane_id() == 0;
@@ -2277,26 +2692,57 @@ constexpr u32 kC3cCap = kC2cCap;
 #endif
 template <class W>
 static hipError_t count3c_w(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                            const Range* rng_ch, const W* mw, PerftResult* res, u32* counter) {
+                            const Range* rng_ch, const W* mw, PerftResult* res, u32* counter, FrontState* fst = nullptr) {
   u32* next = counter ? counter : &res->next_chunk;
   if (stm_g) {
     auto k = k_count3c<1, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
-                       res->divide, next);
+                       res->divide, next, fst);
   } else {
     auto k = k_count3c<0, kC3cCap, DC_C3C_MINW, W>;
     hipLaunchKernelGGL(k, dim3(resident_grid(k, 256, kMaxGrid)), dim3(256), 0, st, nodes, tags, rng, rng_ch, mw,
-                       res->divide, next);
+                       res->divide, next, fst);
   }
   return hipGetLastError();
 }
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
-                          const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter) {
-  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, counter);
+                          const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter, FrontState* fst) {
+  return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, counter, fst);
 }
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
                           const Range* rng_ch, const u64* mw, PerftResult* res, u32* counter) {
   return count3c_w(st, stm_g, nodes, tags, rng, rng_ch, mw, res, counter);
+}
+
+#ifdef DC_AB_KNOBS
+extern "C" __attribute__((visibility("default"))) int dc_ab_front_trace(u64* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_front_trace), sizeof(g_front_trace), 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess
+             ? 0
+             : -1;
+}
+#endif
+
+hipError_t launch_front(hipStream_t st, int stm0, u32 depth, const Board* root, u32 shard, u32 n_shards, Board* out,
+                        uint16_t* out_tags, u32 cap_b, u32* mw, u64 cap_w, PerftResult* res, Range* rng_out,
+                        FrontState* fst) {
+  if (depth != 6 && depth != 7) return hipErrorInvalidValue;
+  // one pass of the resident grid: every block does the top once
+#define DC_FRONT(S, E)                                                                                        \
+  do {                                                                                                        \
+    auto k_ = k_front<S, E>;                                                                                  \
+    hipLaunchKernelGGL(k_, dim3(resident_grid(k_, 256, kMaxGrid)), dim3(256), 0, st, root, shard, n_shards, \
+                       out, out_tags, cap_b, mw, cap_w, res, rng_out, fst);                                   \
+  } while (0)
+  if (depth == 7) {
+    if (stm0) DC_FRONT(1, 1);
+    else DC_FRONT(0, 1);
+  } else {
+    if (stm0) DC_FRONT(1, 0);
+    else DC_FRONT(0, 0);
+  }
+#undef DC_FRONT
+  return hipGetLastError();
 }
 
 // Product: REF -> k_count2c (the bulk split), FIDE -> k_count2b<FideRules>.

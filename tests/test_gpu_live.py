@@ -215,3 +215,54 @@ def test_live_timeout_path_then_fresh_verdicts():
     finally:
         e.live_validator(0)
         e.close()
+
+
+def test_live_calls_beside_device_work_on_another_thread():
+    """a LiveHold on one thread (buffer growth, perft) and live
+    calls on another context in a second thread.  live_call decides under
+    g_live_mu whether a hold is active (dc_api.hip), so no wave is started
+    after a hold has stopped them: every step of the working thread finishes
+    far inside the 20 s lease, and every live verdict stays exact."""
+    import json
+    import os
+    import threading
+    og = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "oracle_golden.json")))
+    want_perft = {d: og["perft_ref"]["startpos"][str(d)]["total"] for d in (3, 4, 5, 6)}
+    pool_pos, pool_mv, pool_want = _pool(27)
+    a, b = dchess.Engine(0), dchess.Engine(0)
+    stop = threading.Event()
+    bad, calls = [], [0]
+
+    def live_loop():
+        rng = np.random.default_rng(27)
+        while not stop.is_set():
+            idx = rng.choice(len(pool_mv), 1 + int(rng.integers(0, 8)), replace=False)
+            got = a.validate_batch(pool_pos[idx], pool_mv[idx])
+            if not (got == pool_want[idx]).all():
+                bad.append(idx)
+            calls[0] += 1
+
+    try:
+        a.live_validator(20_000_000)
+        th = threading.Thread(target=live_loop, daemon=True)
+        th.start()
+        steps = {}
+        for rep in range(3):
+            for d in (3, 4, 5, 6):
+                t0 = time.time()
+                assert b.perft(dchess.startpos(), d)[0] == want_perft[d]
+                steps[f"perft{d}_{rep}"] = time.time() - t0
+            t0 = time.time()
+            mv = b.gen_games(0x5EED + rep, 0, 4096 << rep, 16, 32)  # growing buffers on b
+            b.replay(mv)
+            steps[f"grow_{rep}"] = time.time() - t0
+        stop.set()
+        th.join(10)
+        assert not th.is_alive()
+        assert max(steps.values()) < 5.0, steps
+        assert not bad and calls[0] > 0, (len(bad), calls[0])
+    finally:
+        stop.set()
+        a.live_validator(0)
+        a.close()
+        b.close()

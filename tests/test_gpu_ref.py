@@ -556,6 +556,38 @@ def test_perft6_ref_off_startpos_tree(engine, name):
     assert {m: v for m, v in acc.items() if v} == {m: v for m, v in e["divide"].items() if v}
 
 
+def test_front_path_taken_and_declined(engine):
+    """Round 6's one-launch front end (k_front, dc_perft.hip): REF perft(6) and
+    perft(7) of one root, unsharded or a strided shard of ply 3, run it; a
+    position whose ply 2 is past its LDS bound (pos6 of ref_d6: 2,124 ply-2
+    nodes > 2,048) is declined on the device and rerun on the legacy chain;
+    other shapes (split 4, depth 5, FIDE) never take it.  Totals are the
+    goldens either way (dc_test_perft_last_front reports the path)."""
+    import ctypes as C
+    L = dchess.lib()
+    L.dc_test_perft_last_front.argtypes = [C.c_void_p]
+    front = lambda: L.dc_test_perft_last_front(engine.ctx)  # noqa: E731
+    s = dchess.startpos()
+    for d in (6, 7):
+        for _ in range(2):  # the plain run, then the captured graph
+            assert engine.perft(s, d)[0] == OG["perft_ref"]["startpos"][str(d)]["total"]
+            assert front() == 1
+    t = 0
+    for k in range(8):
+        t += engine.perft_shard(s, 7, 3, k, 8)[0]
+        assert front() == 1
+    assert t == OG["perft_ref"]["startpos"]["7"]["total"]
+    engine.perft_shard(s, 7, 4, 1, 8)
+    assert front() == 0
+    assert engine.perft(s, 5)[0] == OG["perft_ref"]["startpos"]["5"]["total"]
+    assert front() == 0
+    for name, want in (("pos6", 0), ("mid4", 1), ("pos6", 0)):
+        e = REF_D6[name]
+        p = dchess.pos_from_cells(np.array(e["cells"], np.int8), e["stm"])
+        assert engine.perft(p, 6)[0] == e["total"]
+        assert front() == want, name
+
+
 # ------------------------------------------------------------- replicas (C1)
 def test_four_replicas_scripted_game():
     """four in-process replicas (one dc_ctx each, as each

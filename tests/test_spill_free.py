@@ -17,7 +17,7 @@ import dchess
 
 LLVM = "/opt/rocm/lib/llvm/bin"
 # mangled-name fragments of the kernels that must stay spill-free
-MUST = ("k_count3c", "k_count2c", "k_perft_dfs", "k_replay_ref4", "k_validate_ref", "k_apply_ref",
+MUST = ("k_count3c", "k_count2c", "k_front", "k_perft_dfs", "k_replay_ref4", "k_validate_ref", "k_apply_ref",
         "k_gen_games_ref", "RefRules", "FideRules", "k_verify_tx", "k_live")
 
 

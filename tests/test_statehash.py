@@ -136,6 +136,27 @@ def test_state_hash_batch_vs_oracle(engine, case):
 
 
 @pytest.mark.gpu
+def test_state_hash_without_replay_prepass(engine):
+    """when the replay pre-pass's buffers cannot be had (forced here
+    through the test hook dc_test_hash_prepass_max = 0), the hash kernel's own
+    validation path runs instead of the call failing, with the same hashes."""
+    import ctypes as C
+    import oracle_lib as O
+    L = dchess.lib()
+    L.dc_test_hash_prepass_max.argtypes = [C.c_void_p, C.c_uint64]
+    mv = _games(12, 45, 33, O.Pos())
+    names = [(NAMES[g % len(NAMES)], NAMES[(g * 3 + 2) % len(NAMES)] + str(g)) for g in range(45)]
+    with_pre = engine.state_hash(mv, names)
+    try:
+        assert L.dc_test_hash_prepass_max(engine.ctx, 0) == 0
+        without = engine.state_hash(mv, names)
+    finally:
+        L.dc_test_hash_prepass_max(engine.ctx, 2**64 - 1)
+    assert (with_pre == without).all()
+    assert (without == _oracle_hashes(O.Pos(), "", names, mv)).all()
+
+
+@pytest.mark.gpu
 def test_state_hash_matches_gamestate_mirror(engine):
     """One game through the Python GameState mirror (dc_apply_batch per move,
     host JSON + dc_keccak256) and through the batched kernel."""
