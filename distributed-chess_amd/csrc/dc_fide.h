@@ -1,4 +1,4 @@
-// dc_fide.h -- launch wrappers of the RULES_FIDE kernels (dc_fide.hip).
+// dc_fide.h -- launch wrappers of the RULES_FIDE kernels (defined in dc_moves.hip).
 #pragma once
 #include "dc_kernels.h"
 

@@ -767,10 +767,13 @@ __global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ n
 //    first version took both from two global cursors: 768 blocks queued on
 //    them for up to ~15 us, tools/front_trace.py) -- so both levels come out
 //    in the canonical order of the legacy chain.
-//  * Every serial walk is split over the four class groups of
+//  * The top's serial walks are split over the four class groups of
 //    ref_group_moves, one wave per group (a lane walks a quarter of a
-//    position's moves): one lane walking ~25 moves was ~7 us of the first
-//    version's ~30 us per item.
+//    position's moves; one lane walking ~25 moves was ~7 us of the first
+//    version's ~30 us per item).  The item's words are not: pawn moves are
+//    ~60 % of them, and every block's wave 0 sits on SIMD 0, so wave = group
+//    left three SIMDs idle (~6 us per 2,048-word window, front_trace.py).
+//    There one lane walks one board, boards dealt round-robin over the waves.
 //  * The block holding the last item publishes the two Ranges (or, when a
 //    level is past its capacity or the top past the LDS bounds, flags
 //    overflow + front_declined: the host reruns on the legacy chain).  Block
@@ -779,13 +782,12 @@ constexpr u32 kFrontPly1Max = 128;    // root moves (more: the legacy chain)
 constexpr u32 kFrontPly2Max = 2048;   // ply-2 nodes (more: the legacy chain)
 constexpr u32 kFrontP3Max = 64;       // ply-3 nodes per item
 constexpr u32 kFrontBoardsMax = 1024; // boards per item (more: declined)
-constexpr u32 kFrontSlotW = 2048;     // move-word slots of one window
 
 #ifdef DC_AB_KNOBS
 // A/B build: k_front's timeline (wall clock, 100 MHz) for the first
 // kFrontTraceBlocks blocks: kFrontTraceWords stamps each, read back by
 // dc_ab_front_trace (tools/front_trace.py).
-constexpr u32 kFrontTraceBlocks = 64, kFrontTraceWords = 16;
+constexpr u32 kFrontTraceBlocks = 2048, kFrontTraceWords = 16;
 __device__ u64 g_front_trace[kFrontTraceBlocks * kFrontTraceWords];
 #define DC_FRONT_STAMP(k)                                                                     \
   do {                                                                                        \
@@ -798,10 +800,20 @@ __device__ u64 g_front_trace[kFrontTraceBlocks * kFrontTraceWords];
   } while (0)
 #endif
 
-struct FrontShared {
+struct FrontTop {            // the top, rebuilt by every block (front_top)
   Board p1[kFrontPly1Max];
   u32 w2[kFrontPly2Max];     // ply-2 nodes: ply-1 index << 12 | f | t << 6
   u32 off3[kFrontPly2Max];   // their ply-3 move counts, then exclusive offsets
+};
+constexpr u32 kFrontWin = sizeof(FrontTop) / sizeof(u32);  // move words of one window (5,120)
+
+struct FrontShared {
+  // The word windows overlay the top: it is dead once an item's ply-3 nodes
+  // are selected, and a block holding a further item rebuilds it.
+  union {
+    FrontTop top;
+    u32 slotw[kFrontWin];
+  };
   Board b2[kFrontP3Max];     // an item's ply-3 nodes' parents
   Board b3[kFrontP3Max];     // an item's ply-3 nodes
   u32 r3[kFrontP3Max];       // ... their rank among the parent's moves
@@ -809,15 +821,14 @@ struct FrontShared {
   uint16_t m1[kFrontPly1Max];
   u32 gc[4][kFrontPly1Max];  // per-group move counts (ply 2, selection, ply 4)
   u32 noff[kFrontPly1Max];   // per-node move offsets (ply 2, ply 4)
-  u32 slot4[kFrontBoardsMax];            // E = 1: an item's ply-4 moves (ply-3 node << 12 | f | t << 6)
-  uint16_t gw[4][kFrontBoardsMax];       // per-(group, board) word counts
-  u32 woff[kFrontBoardsMax];             // per-board word offsets
-  u32 slotw[kFrontSlotW];                // move words of one window
+  u32 slot4[kFrontBoardsMax];         // E = 1: an item's ply-4 moves (ply-3 node << 12 | f | t << 6)
+  uint16_t wc[kFrontBoardsMax];       // per-board word counts
+  uint16_t gw[4][kFrontP3Max];        // per-(group, board) word counts (items of <= 64 boards)
+  u32 woff[kFrontBoardsMax];          // per-board word offsets
   u64 red[4][3];
-  u64 look[3];
   u32 g1[4];
   u32 wsum[4];
-  u32 n4, bad, jm;
+  u32 jm;
 };
 
 // Per item: the published aggregate and inclusive prefix (FrontState, dc_perft.h),
@@ -866,36 +877,54 @@ __device__ __forceinline__ void front_block_sum(FrontShared& sh, u64& bad, u64& 
 }
 
 // Decoupled look-back: the (bad, boards, words) of items [0, it), read
-// backwards in windows of 256 items; a window holding an inclusive prefix
-// ends the walk.  Every earlier item is held by a resident block that takes
-// its items in increasing order, so every slot waited on is written.  The
-// slots carry all the data exchanged, so the loads and stores are relaxed
-// device-scope atomics: acquire / release forms add a cache invalidate or
-// write-back per access (a spinning first version spent ~30 us here).
+// backwards in windows of 1,024 items (4 per thread); a window holding an
+// inclusive prefix ends the walk.  Every earlier item is held by a resident
+// block that takes its items in increasing order, so every slot waited on is
+// written.  The slots carry all the data exchanged, so the loads and stores
+// are relaxed device-scope atomics: acquire / release forms add a cache
+// invalidate or write-back per access (a spinning first version spent ~30 us
+// here).
+constexpr u32 kFrontLook = 4;
 __device__ __forceinline__ void front_lookback(FrontShared& sh, FrontState* st, u32 it, u64& bad, u64& nb, u64& nw) {
   const u32 t = threadIdx.x;
   bad = nb = nw = 0;
   u32 hi = it;
   while (hi > 0) {  // block-uniform
-    const u32 lo = hi > 256 ? hi - 256 : 0u;
-    const u32 j = lo + t;
-    u64 a = 0, inc = 0;
-    if (j < hi) {
-      do {
-        a = __hip_atomic_load(&st->agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } while (!(a >> 63));
-      inc = __hip_atomic_load(&st->incl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 lo = hi > 256 * kFrontLook ? hi - 256 * kFrontLook : 0u;
+    u64 a[kFrontLook], inc[kFrontLook];
+#pragma unroll
+    for (u32 r = 0; r < kFrontLook; ++r) {
+      const u32 j = lo + r * 256 + t;
+      a[r] = inc[r] = 0;
+      if (j < hi) {
+        for (;;) {
+          a[r] = __hip_atomic_load(&st->agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (a[r] >> 63) break;
+          __builtin_amdgcn_s_sleep(2);  // (backoff: ~128 cycles between polls of a slot not yet written)
+        }
+        inc[r] = __hip_atomic_load(&st->incl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
-    const bool has_inc = j < hi && (inc >> 63);
     if (t == 0) sh.jm = 0;
     __syncthreads();
-    if (has_inc) atomicMax(&sh.jm, j + 1);  // the last inclusive prefix of the window (+1)
+#pragma unroll
+    for (u32 r = 0; r < kFrontLook; ++r) {
+      const u32 j = lo + r * 256 + t;
+      if (j < hi && (inc[r] >> 63)) atomicMax(&sh.jm, j + 1);  // the window's last inclusive prefix (+1)
+    }
     __syncthreads();
     const u32 jm = sh.jm;  // 0: none in this window
-    u64 v = 0;
-    if (jm && j == jm - 1) v = inc;
-    else if (j < hi && (!jm || j >= jm)) v = a;
-    u64 b1 = (v >> 62) & 1, n1 = (v >> 40) & 0x3FFFFFull, w1 = v & 0xFFFFFFFFFFull;
+    u64 b1 = 0, n1 = 0, w1 = 0;
+#pragma unroll
+    for (u32 r = 0; r < kFrontLook; ++r) {
+      const u32 j = lo + r * 256 + t;
+      u64 v = 0;
+      if (jm && j == jm - 1) v = inc[r];
+      else if (j < hi && (!jm || j >= jm)) v = a[r];
+      b1 |= (v >> 62) & 1;
+      n1 += (v >> 40) & 0x3FFFFFull;
+      w1 += v & 0xFFFFFFFFFFull;
+    }
     front_block_sum(sh, b1, n1, w1);
     bad |= b1 ? 1ull : 0ull;
     nb += n1;
@@ -923,71 +952,72 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     for (u32 k = t; k < sizeof(PerftResult) / 8; k += 256) reinterpret_cast<u64*>(res)[k] = 0;
   }
   const Board root = root_p[0];
-  // ---- ply 1: wave g counts and walks class group g of the root
-  if (lane == 0) sh.g1[wave] = front_group_count<S0>(wave, root);
-  __syncthreads();
-  const u32 n1 = sh.g1[0] + sh.g1[1] + sh.g1[2] + sh.g1[3];
-  bool ok = n1 <= kFrontPly1Max;  // block-uniform from here on
-  if (ok && lane == 0) {
-    u32 j = 0;
-    for (u32 g = 0; g < wave; ++g) j += sh.g1[g];
-    front_group_moves<S0>(wave, root, [&](int f, int to) { sh.m1[j++] = (uint16_t)(f | (to << 6)); });
-  }
-  __syncthreads();
-  if (ok && t < n1) {
-    const u32 m = sh.m1[t];
-    Board b = root;
-    ref_make(b, (int)(m & 63), (int)(m >> 6));
-    sh.p1[t] = b;
-    if (blockIdx.x == 0) res->root_moves[t] = (uint16_t)m;  // (after the clear: barriers between)
-  }
-  __syncthreads();
-  DC_FRONT_STAMP(1);
-  // ---- ply 2: wave w takes class group w of nodes lane and 64 + lane
-  u32 n2 = 0;
-  if (ok) {
+  u32 n1 = 0, n2 = 0, n3 = 0;
+  // The top: plies 1 and 2 and the ply-3 offsets of the ply-2 nodes in LDS.
+  // Returns false when it does not fit (block-uniform).  Block 0 records the
+  // root moves (after the clear: barriers between).
+  auto front_top = [&](bool record) -> bool {
+    // ply 1: wave g counts and walks class group g of the root
+    if (lane == 0) sh.g1[wave] = front_group_count<S0>(wave, root);
+    __syncthreads();
+    n1 = sh.g1[0] + sh.g1[1] + sh.g1[2] + sh.g1[3];
+    if (n1 > kFrontPly1Max) return false;
+    if (lane == 0) {
+      u32 j = 0;
+      for (u32 g = 0; g < wave; ++g) j += sh.g1[g];
+      front_group_moves<S0>(wave, root, [&](int f, int to) { sh.m1[j++] = (uint16_t)(f | (to << 6)); });
+    }
+    __syncthreads();
+    if (t < n1) {
+      const u32 m = sh.m1[t];
+      Board b = root;
+      ref_make(b, (int)(m & 63), (int)(m >> 6));
+      sh.top.p1[t] = b;
+      if (record) res->root_moves[t] = (uint16_t)m;
+    }
+    __syncthreads();
+    DC_FRONT_STAMP(1);
+    // ply 2: wave w takes class group w of nodes lane and 64 + lane
     for (u32 node = lane; node < kFrontPly1Max; node += 64)
-      sh.gc[wave][node] = node < n1 ? front_group_count<S1>(wave, sh.p1[node]) : 0u;
+      sh.gc[wave][node] = node < n1 ? front_group_count<S1>(wave, sh.top.p1[node]) : 0u;
     __syncthreads();
     const u32 tot = t < kFrontPly1Max ? sh.gc[0][t] + sh.gc[1][t] + sh.gc[2][t] + sh.gc[3][t] : 0u;
     const u32 ex = block_excl_scan32<4>(tot, sh.wsum, &n2);
     if (t < kFrontPly1Max) sh.noff[t] = ex;
-    ok = n2 <= kFrontPly2Max;
     __syncthreads();
-  }
-  DC_FRONT_STAMP(2);
-  if (ok) {
+    DC_FRONT_STAMP(2);
+    if (n2 > kFrontPly2Max) return false;
     for (u32 node = lane; node < n1; node += 64) {
       u32 j = sh.noff[node];
       for (u32 g = 0; g < wave; ++g) j += sh.gc[g][node];
-      front_group_moves<S1>(wave, sh.p1[node], [&](int f, int to) { sh.w2[j++] = (node << 12) | (u32)f | ((u32)to << 6); });
+      front_group_moves<S1>(wave, sh.top.p1[node],
+                            [&](int f, int to) { sh.top.w2[j++] = (node << 12) | (u32)f | ((u32)to << 6); });
     }
     __syncthreads();
-  }
-  DC_FRONT_STAMP(3);
-  // ---- ply-3 counts of the ply-2 nodes, scanned in place into offsets
-  u32 n3 = 0;
-  if (ok) {
+    DC_FRONT_STAMP(3);
+    // ply-3 counts of the ply-2 nodes, scanned in place into offsets
     for (u32 j = t; j < n2; j += 256) {
-      const u32 e = sh.w2[j];
-      Board b = sh.p1[e >> 12];
+      const u32 e = sh.top.w2[j];
+      Board b = sh.top.p1[e >> 12];
       ref_make(b, (int)(e & 63), (int)((e >> 6) & 63));
-      sh.off3[j] = ref_count<S0>(b);
+      sh.top.off3[j] = ref_count<S0>(b);
     }
     __syncthreads();
     DC_FRONT_STAMP(4);
     const u32 seg = (n2 + 255) / 256, a = min(n2, t * seg), z = min(n2, a + seg);
     u32 s = 0;
-    for (u32 j = a; j < z; ++j) s += sh.off3[j];
+    for (u32 j = a; j < z; ++j) s += sh.top.off3[j];
     u32 run = block_excl_scan32<4>(s, sh.wsum, &n3);
     for (u32 j = a; j < z; ++j) {
-      const u32 v = sh.off3[j];
-      sh.off3[j] = run;
+      const u32 v = sh.top.off3[j];
+      sh.top.off3[j] = run;
       run += v;
     }
     __syncthreads();
-  }
-  DC_FRONT_STAMP(5);
+    DC_FRONT_STAMP(5);
+    return true;
+  };
+  const bool ok = front_top(blockIdx.x == 0);
   if (blockIdx.x == 0 && t == 0) {
     res->n_root = n1;
     res->level_n[1] = n1;
@@ -1000,7 +1030,7 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
   P3 = min(kFrontP3Max, max(P3, (m3 + kFrontItemsMax - 1) / kFrontItemsMax));
   const u32 n_items = (m3 + P3 - 1) / P3;
   if (blockIdx.x == 0 && t == 0) st->n_items = n_items;  // (k_count3c clears that many slots)
-  if (!ok || (n_items == 0 && blockIdx.x == 0)) {  // nothing to expand: block 0 publishes the result
+  if (!ok || n_items == 0) {  // nothing to expand: block 0 publishes the result
     if (blockIdx.x == 0 && t == 0) {
       if (!ok) {
         res->overflow = 1;
@@ -1012,6 +1042,7 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     return;
   }
   for (u32 it = blockIdx.x; it < n_items; it += gridDim.x) {
+    if (it != blockIdx.x) (void)front_top(false);  // the previous item's words overwrote it
     const u32 k0 = it * P3, np3 = min(P3, m3 - k0);
     // -- select the item's ply-3 nodes: parent by binary search (wave 0), the
     //    rank's class group by one group count per wave, the move by one walk
@@ -1020,14 +1051,14 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
       u32 lo = 0, hi = n2;  // the last ply-2 node whose offset is <= q (it has q's move)
       while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
-        if (sh.off3[mid] <= q) lo = mid;
+        if (sh.top.off3[mid] <= q) lo = mid;
         else hi = mid;
       }
-      const u32 e = sh.w2[lo];
-      Board b2 = sh.p1[e >> 12];
+      const u32 e = sh.top.w2[lo];
+      Board b2 = sh.top.p1[e >> 12];
       ref_make(b2, (int)(e & 63), (int)((e >> 6) & 63));
       sh.b2[lane] = b2;
-      sh.r3[lane] = q - sh.off3[lo];
+      sh.r3[lane] = q - sh.top.off3[lo];
       sh.t3[lane] = (uint16_t)(e >> 12);
     }
     __syncthreads();
@@ -1085,56 +1116,96 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
         return sh.b3[k];
       }
     };
-    // -- pass 1: per-(group, board) word counts, per-board offsets
-    for (u32 k = lane; k < nbd; k += 64) sh.gw[wave][k] = (uint16_t)front_group_count<SF>(wave, board_at(k));
+    // -- pass 1: word counts.  Up to 64 boards: per (group, board), wave g
+    //    taking group g (a lane walks a quarter of a board later); more: per
+    //    board, boards dealt round-robin over the waves (k % 4 = wave).
+    const bool split = nbd <= kFrontP3Max;  // block-uniform
+    if (split) {
+      if (lane < nbd) sh.gw[wave][lane] = (uint16_t)front_group_count<SF>(wave, board_at(lane));
+      __syncthreads();
+      if (t < nbd) sh.wc[t] = (uint16_t)(sh.gw[0][t] + sh.gw[1][t] + sh.gw[2][t] + sh.gw[3][t]);
+    } else {
+      for (u32 k = wave + 4 * lane; k < nbd; k += 256) sh.wc[k] = (uint16_t)ref_count<SF>(board_at(k));
+    }
     __syncthreads();
     const u32 seg = (nbd + 255) / 256, a = min(nbd, t * seg), z = min(nbd, a + seg);
     u32 s = 0;
-    for (u32 k = a; k < z; ++k) s += (u32)sh.gw[0][k] + sh.gw[1][k] + sh.gw[2][k] + sh.gw[3][k];
+    for (u32 k = a; k < z; ++k) s += sh.wc[k];
     u32 nw;
     u32 run = block_excl_scan32<4>(s, sh.wsum, &nw);
     for (u32 k = a; k < z; ++k) {
       sh.woff[k] = run;
-      run += (u32)sh.gw[0][k] + sh.gw[1][k] + sh.gw[2][k] + sh.gw[3][k];
+      run += sh.wc[k];
     }
-    // -- publish, look back, publish the inclusive prefix
-    if (t == 0) {
+    // -- publish the item's counts, walk its words into the first LDS window
+    //    (board index relative to the item, rebased when stored), then look
+    //    back: a block waiting on a slower predecessor has its walk done
+    if (t == 0)
       __hip_atomic_store(&st->agg[it], front_pack(bad, nbd, nw), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+#ifdef DC_AB_KNOBS
+    if (it == blockIdx.x) DC_FRONT_STAMP(12);
+#endif
+    __syncthreads();  // woff / wc
+    auto walk = [&](u32 wb) {  // the words [wb, wb + kFrontWin) into slotw
+      if (split) {
+        if (lane < nbd) {
+          u32 j = sh.woff[lane];
+          for (u32 g = 0; g < wave; ++g) j += sh.gw[g][lane];
+          const u32 c = sh.gw[wave][lane];
+          if (c && j < wb + kFrontWin && j + c > wb)
+            front_group_moves<SF>(wave, board_at(lane), [&](int f, int to) {
+              if (j >= wb && j - wb < kFrontWin) sh.slotw[j - wb] = (lane << 12) | (u32)f | ((u32)to << 6);
+              ++j;
+            });
+        }
+      } else {
+        for (u32 k = wave + 4 * lane; k < nbd; k += 256) {
+          u32 j = sh.woff[k];
+          const u32 c = sh.wc[k];
+          if (c && j < wb + kFrontWin && j + c > wb)
+            ref_for_each_move<SF>(board_at(k), [&](int f, int to) {
+              if (j >= wb && j - wb < kFrontWin) sh.slotw[j - wb] = (k << 12) | (u32)f | ((u32)to << 6);
+              ++j;
+            });
+        }
+      }
+      __syncthreads();
+    };
+    if (nw) walk(0);
+#ifdef DC_AB_KNOBS
+    if (it == blockIdx.x) DC_FRONT_STAMP(11);
+#endif
     u64 pbad, pb, pw;
-    front_lookback(sh, st, it, pbad, pb, pw);  // (its barriers publish woff)
-    if (t == 0) {
+    front_lookback(sh, st, it, pbad, pb, pw);
+    if (t == 0)
       __hip_atomic_store(&st->incl[it], front_pack(pbad | bad, pb + nbd, pw + nw), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    }
     if (it == blockIdx.x) DC_FRONT_STAMP(8);
     const u64 base_b = pb, base_w = pw;
     const bool fits = !pbad && !bad && base_b + nbd <= cap_b;  // (else flagged below: no store)
-    // -- pass 2: the boards, then the words through LDS windows
+    // -- the boards, then the words window by window
     if (fits)
       for (u32 k = t; k < nbd; k += 256) {
         store_board(out, base_b + k, board_at(k));
         out_tags[base_b + k] = E == 1 ? sh.t3[sh.slot4[k] >> 12] : sh.t3[k];
       }
-    for (u32 wb = 0; fits && wb < nw; wb += kFrontSlotW) {  // block-uniform
-      if (wb) __syncthreads();  // the previous window is stored
-      for (u32 k = lane; k < nbd; k += 64) {
-        u32 j = sh.woff[k];
-        for (u32 g = 0; g < wave; ++g) j += sh.gw[g][k];
-        const u32 c = sh.gw[wave][k];
-        if (c && j < wb + kFrontSlotW && j + c > wb) {
-          const u32 gidx = (u32)(base_b + k);
-          front_group_moves<SF>(wave, board_at(k), [&](int f, int to) {
-            if (j >= wb && j - wb < kFrontSlotW) sh.slotw[j - wb] = (gidx << 12) | (u32)f | ((u32)to << 6);
-            ++j;
-          });
-        }
+#ifdef DC_AB_KNOBS
+    if (it == blockIdx.x && t == 0 && blockIdx.x < kFrontTraceBlocks) {
+      g_front_trace[blockIdx.x * kFrontTraceWords + 13] = nw;
+      g_front_trace[blockIdx.x * kFrontTraceWords + 14] = nbd;
+    }
+    if (it == blockIdx.x) DC_FRONT_STAMP(10);
+#endif
+    const u32 rebase = (u32)base_b << 12;
+    for (u32 wb = 0; fits && wb < nw; wb += kFrontWin) {  // block-uniform
+      if (wb) {
+        __syncthreads();  // the previous window is stored
+        walk(wb);
       }
-      __syncthreads();
-      const u32 ns = min(kFrontSlotW, nw - wb);
+      const u32 ns = min(kFrontWin, nw - wb);
       for (u32 r = t; r < ns; r += 256) {
         const u64 o = base_w + wb + r;
-        if (o < cap_w) mw[o] = sh.slotw[r];
+        if (o < cap_w) mw[o] = sh.slotw[r] + rebase;
       }
     }
     if (it == blockIdx.x) DC_FRONT_STAMP(9);
@@ -1151,7 +1222,7 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
         rng_out[1] = Range{0, tw};
       }
     }
-    __syncthreads();  // the item's LDS is reused by the next item
+    __syncthreads();  // the item's LDS (and the windows over the top) is reused by the next item
   }
 }
 

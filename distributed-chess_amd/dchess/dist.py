@@ -2,9 +2,10 @@
 
 Perft.  Every rank rebuilds the top plies identically (their order is
 deterministic) and counts the subtrees of its STRIDED shard of the ply-`split`
-frontier: nodes rank, rank + world, rank + 2*world, ... (dc_perft_shard,
-k_gather_shard; strided shards carry equal leaf counts to ~1 %, contiguous
-eighths differed by 1.47x).  The per-root-move divide vectors are summed with
+frontier: nodes rank, rank + world, rank + 2*world, ... (dc_perft_shard: the
+front end selects the shard's nodes by index -- k_front for REF depth 6/7 at
+split 3, k_make_count over the top kernel's move words otherwise; strided
+shards carry equal leaf counts to ~1 %, contiguous eighths differed by 1.47x).  The per-root-move divide vectors are summed with
 one all-reduce -- RCCL over xGMI with the "nccl" backend, gloo on CPU in the
 tests.  (The A/B build's DC_SHARD=contig knob takes contiguous slices.)
 

@@ -303,9 +303,11 @@ int dc_perft(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uin
 /* One shard of perft for data-parallel runs: the frontier at ply `split_depth`
  * (N nodes) is built deterministically, and this call counts only the subtrees
  * of the STRIDED shard of it -- frontier nodes shard, shard + n_shards,
- * shard + 2*n_shards, ... < N (k_gather_shard; strided shards hold equal leaf
- * counts to about 1 %, contiguous ones did not).  Summing divide[] over all
- * shards (e.g. an RCCL all-reduce) gives dc_perft's result exactly. */
+ * shard + 2*n_shards, ... < N (the front end selects them by index: REF depth
+ * 6/7 at split 3 in k_front, else k_make_count over the top kernel's move
+ * words; strided shards hold equal leaf counts to about 1 %, contiguous ones
+ * did not).  Summing divide[] over all shards (e.g. an RCCL all-reduce) gives
+ * dc_perft's result exactly. */
 int dc_perft_shard(dc_ctx* ctx, uint32_t rules, const dc_pos* pos, uint32_t depth, uint32_t split_depth,
                    uint32_t shard, uint32_t n_shards, uint64_t* divide, uint16_t* root_moves,
                    uint32_t* n_root, uint64_t* total);
