@@ -258,7 +258,7 @@ def enqueue_split(engs, steps, base_ptr, W, fn):
         e.synchronize()
 
 
-def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF, want=None):
+def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF, want=None, streams=None):
     """warmup + exactly `steps` timed perft(depth) steps (barrier + device sync on
     both sides, max over ranks), parity-checked against the golden count.
 
@@ -279,7 +279,8 @@ def timed_perft(eng, d, args, pos, depth, steps, warmup, rules=dchess.RULES_REF,
     # the first dc_perft_repeat_device call of a configuration runs one plain
     # perft and captures the launch graphs (one run, and a batch of
     # REPEAT_BATCH runs): do it here, outside the timed region
-    engs = perft_contexts(eng, d, max(1, min(perft_streams(args, depth, d.world), steps)))
+    n_ctx = streams if streams is not None else perft_streams(args, depth, d.world)
+    engs = perft_contexts(eng, d, max(1, min(n_ctx, steps)))
     share = -(-steps // len(engs))
     warm = eng.alloc(REPEAT_BATCH * W * 8)
     for e in engs:  # every context captures its graphs (one run; a batch of REPEAT_BATCH when its share has one)
@@ -340,7 +341,8 @@ def profiled_perft(eng, d, args, pos, depth, steps):
         perft_step(eng, d, args, pos, depth)
     d.sync()
     eng.set_profiling(False)
-    return {k: eng.kernel_stats(k) for k in ("expand_top", "expand_count", "scan", "expand_write", "level_moves", "count2")}
+    return {k: eng.kernel_stats(k) for k in ("front", "expand_top", "expand_count", "scan", "expand_write", "level_moves",
+                                             "count2")}
 
 
 def _pmc(key):
@@ -1030,6 +1032,15 @@ def main():
         p6 = {"value": l6 / dt6, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt6 / (4 * args.steps),
               "steps": 4 * args.steps, "workload": "perft(startpos, 6) RULES_REF, frontier split at ply 3",
               "scaling": "strong", "streams_per_gpu": perft_streams(args, 6, d.world)}
+    # one context (stream) per GPU: one run's latency, its front end not hidden
+    # behind another run's final stage (the like-for-like figure)
+    one = None
+    if "perft" in legs and (not args.profile_only or args.only):
+        note("perft_one_stream")
+        one = {}
+        for dd, k in ((args.depth, args.steps), (6, 4 * args.steps)):
+            l1, dt1 = timed_perft(eng, d, args, pos, dd, k, args.warmup, streams=1)
+            one[f"perft{dd}"] = {"value": l1 / dt1, "unit": "leaf nodes/s", "ms_per_step": 1e3 * dt1 / k, "steps": k}
     if "perft8" in legs:
         note("perft8")
         p8 = perft8_leg(eng, d, args, pos)
@@ -1087,6 +1098,8 @@ def main():
     if ks is not None:
         line["roofline"] = roofline(ks, args.depth, d.world)
         line["kernels_ms_per_step"] = {k: v["total_ms"] / args.steps for k, v in ks.items()}
+    if one is not None:
+        line["perft_one_stream"] = one
     if p8 is not None:
         line["perft8"] = p8
     if p9 is not None:

@@ -206,6 +206,7 @@ struct dc_ctx {
   DBuf<u32> slice_ctr;        // ... and its group counter
   DBuf<u32> top_words;   // k_expand_top's last ply as move words (k_make_count makes it)
   DBuf<uint8_t> front_st;  // k_front's look-back slots, a dc::FrontState (zeroed once; k_count3c re-zeroes them)
+  DBuf<u32> front_spill;   // k_front's spill rows (items past one LDS window)
   uint8_t* front_st_zeroed = nullptr;
   // transaction-signature check: staged strings / offsets / actions / turns,
   // and the G table (built on first use)
@@ -236,6 +237,7 @@ struct dc_ctx {
     desc.release();
     top_words.release();
     front_st.release();
+    front_spill.release();
     move_words.release();
     dfs_stack.release();
     move_words64.release();
@@ -1491,6 +1493,7 @@ static int front_enqueue(dc_ctx* c, const dc_pos* pos, uint32_t depth, uint32_t 
   int e = ensure_level(c, 0, cap_b, false);
   if (e != DC_SUCCESS) return e;
   HIP_TRY(c->move_words.ensure(cap_w));
+  HIP_TRY(c->front_spill.ensure(dc::front_spill_words()));
   if (stage_root) {
     e = write_root_host(c, pos, 1);
     if (e == DC_SUCCESS) e = upload_roots(c, 1, false);
@@ -1499,7 +1502,7 @@ static int front_enqueue(dc_ctx* c, const dc_pos* pos, uint32_t depth, uint32_t 
   dc::Range* rng = c->rng.p + 8;  // [8] the grandparents, [9] the move words
   HIP_TRY(c->timed("front", 0, [&] {
     return dc::launch_front(c->stream, pos->stm, depth, c->root.p, shard, n_shards, c->nodes[0].p, c->tags[0].p,
-                            cap_b, c->move_words.p, cap_w, c->res.p, rng, fst);
+                            cap_b, c->move_words.p, cap_w, c->res.p, rng, fst, c->front_spill.p);
   }));
   c->last_final = "count2";
   const int stm_g = pos->stm ^ (int)((depth - 3) & 1);  // the grandparents are ply depth - 3

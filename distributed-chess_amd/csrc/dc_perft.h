@@ -108,7 +108,9 @@ hipError_t launch_level_moves(hipStream_t st, int stm, const Board* nodes, const
                               const u32* counts, const u64* chunk_base, u32* mw, u64 mw_cap);
 struct FrontState;
 // fst != nullptr (after launch_front): the front end's look-back slots are
-// cleared for the next run.
+// cleared for the next run.  (Round 6 also tried the run's result record
+// written by the last block to finish instead of k_copy_result: a done
+// counter and a device fence per block cost more than the launch.)
 hipError_t launch_count3c(hipStream_t st, int stm_g, const Board* nodes, const uint16_t* tags, const Range* rng,
                           const Range* rng_ch, const u32* mw, PerftResult* res, u32* counter = nullptr,
                           FrontState* fst = nullptr);
@@ -142,9 +144,12 @@ struct FrontState {
   u64 agg[kFrontItemsMax];
   u64 incl[kFrontItemsMax];
 };
+// spill (front_spill_words() u32, or null): per-item rows for the words of
+// items past one LDS window (no second walk).
+u64 front_spill_words();
 hipError_t launch_front(hipStream_t st, int stm0, u32 depth, const Board* root, u32 shard, u32 n_shards, Board* out,
                         uint16_t* out_tags, u32 cap_b, u32* mw, u64 cap_w, PerftResult* res, Range* rng_out,
-                        FrontState* fst);
+                        FrontState* fst, u32* spill);
 
 // K4 (REF): per-lane DFS over L plies below the frontier level `rng` (1 <= L <= 3),
 // each level-L node bulk-counted over the last two plies (perft depth = frontier

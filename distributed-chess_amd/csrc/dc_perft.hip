@@ -754,39 +754,46 @@ __global__ __launch_bounds__(256) void k_level_moves(const Board* __restrict__ n
 // k_chunk_scan, k_level_write, k_chunk_scan and k_level_moves (~67 us of
 // dependent, latency-bound launches per run, round 5).
 //
-//  * Every block rebuilds plies 1 and 2 and the ply-3 move counts of the ply-2
-//    nodes in LDS (a few hundred nodes: cheaper than a launch and a global
-//    round trip), so every block knows the canonical ply-3 order -- ply-1
-//    parents in order, ref_for_each_move's class-major order within a parent
-//    -- that the strided shards of dc_perft_shard are cut from.
+//  * One 1024-thread block per CU.  Every block rebuilds plies 1 and 2 and
+//    the ply-3 move counts of the ply-2 nodes in LDS (a few hundred nodes:
+//    cheaper than a launch and a global round trip), so every block knows the
+//    canonical ply-3 order -- ply-1 parents in order, ref_for_each_move's
+//    class-major order within a parent -- that the strided shards of
+//    dc_perft_shard are cut from.  (Four 256-thread blocks per CU rebuilt the
+//    top four times per CU, and the fourth, whose waves lose the SIMDs'
+//    oldest-first arbitration, finished last: tools/front_trace.py.)
 //  * Items of P3 consecutive ply-3 nodes of this rank's shard (P3 sized so one
-//    pass of the resident grid covers the shard) are expanded E plies (0:
-//    perft(6), 1: perft(7)); the boards and their move words are counted
-//    first, and the item's offsets come from a decoupled look-back over the
-//    earlier items' published (boards, words) -- no same-address atomics (a
-//    first version took both from two global cursors: 768 blocks queued on
-//    them for up to ~15 us, tools/front_trace.py) -- so both levels come out
-//    in the canonical order of the legacy chain.
-//  * The top's serial walks are split over the four class groups of
-//    ref_group_moves, one wave per group (a lane walks a quarter of a
-//    position's moves; one lane walking ~25 moves was ~7 us of the first
-//    version's ~30 us per item).  The item's words are not: pawn moves are
-//    ~60 % of them, and every block's wave 0 sits on SIMD 0, so wave = group
-//    left three SIMDs idle (~6 us per 2,048-word window, front_trace.py).
-//    There one lane walks one board, boards dealt round-robin over the waves.
+//    pass of the grid covers the shard) are expanded E plies (0: perft(6),
+//    1: perft(7)); the boards and their move words are counted first, and the
+//    item's offsets come from a decoupled look-back over the earlier items'
+//    published (boards, words) -- no same-address atomics (a first version
+//    took both from two global cursors: 768 blocks queued on them for up to
+//    ~15 us) -- so both levels come out in the canonical order of the legacy
+//    chain.  The item's words are walked into an LDS window (board index
+//    relative to the item) before the look-back and rebased when stored.
+//  * Every serial walk is split over the four class groups of
+//    ref_group_moves (a lane walks a quarter of a position's moves).  Group g
+//    is taken by waves 4g .. 4g + 3, which sit on the four SIMDs, so each SIMD
+//    holds one wave of each group: pawn moves are ~60 % of the words, and a
+//    group-per-SIMD mapping (group = wave % 4) left three SIMDs mostly idle.
 //  * The block holding the last item publishes the two Ranges (or, when a
 //    level is past its capacity or the top past the LDS bounds, flags
 //    overflow + front_declined: the host reruns on the legacy chain).  Block
 //    0 clears the run's result block and records the root moves.
-constexpr u32 kFrontPly1Max = 128;    // root moves (more: the legacy chain)
-constexpr u32 kFrontPly2Max = 2048;   // ply-2 nodes (more: the legacy chain)
-constexpr u32 kFrontP3Max = 64;       // ply-3 nodes per item
-constexpr u32 kFrontBoardsMax = 1024; // boards per item (more: declined)
+constexpr u32 kFrontThreads = 1024, kFrontWaves = kFrontThreads / 64;
+constexpr u32 kFrontPly1Max = 128;     // root moves (more: the legacy chain)
+constexpr u32 kFrontPly2Max = 2048;    // ply-2 nodes (more: the legacy chain)
+constexpr u32 kFrontP3Max = 128;       // ply-3 nodes per item
+constexpr u32 kFrontBoardsMax = 2048;  // boards per item (more: declined)
+constexpr u32 kFrontWin = 28672;       // move words of one LDS window (112 KB: startpos perft(7) items
+                                       // hold 12k-32k words)
+constexpr u32 kFrontSpillItems = 1024; // items with a spill row for a second window
+constexpr u32 kFrontChunk = 5;         // consecutive ply-3 nodes per chunk of an item
 
 #ifdef DC_AB_KNOBS
-// A/B build: k_front's timeline (wall clock, 100 MHz) for the first
-// kFrontTraceBlocks blocks: kFrontTraceWords stamps each, read back by
-// dc_ab_front_trace (tools/front_trace.py).
+// A/B build: k_front's timeline (wall clock, 100 MHz) per block:
+// kFrontTraceWords stamps each, read back by dc_ab_front_trace
+// (tools/front_trace.py).
 constexpr u32 kFrontTraceBlocks = 2048, kFrontTraceWords = 16;
 __device__ u64 g_front_trace[kFrontTraceBlocks * kFrontTraceWords];
 #define DC_FRONT_STAMP(k)                                                                     \
@@ -805,29 +812,31 @@ struct FrontTop {            // the top, rebuilt by every block (front_top)
   u32 w2[kFrontPly2Max];     // ply-2 nodes: ply-1 index << 12 | f | t << 6
   u32 off3[kFrontPly2Max];   // their ply-3 move counts, then exclusive offsets
 };
-constexpr u32 kFrontWin = sizeof(FrontTop) / sizeof(u32);  // move words of one window (5,120)
+static_assert(sizeof(FrontTop) <= kFrontWin * sizeof(u32), "the window covers the top");
 
 struct FrontShared {
-  // The word windows overlay the top: it is dead once an item's ply-3 nodes
+  // The word window overlays the top: it is dead once an item's ply-3 nodes
   // are selected, and a block holding a further item rebuilds it.
   union {
     FrontTop top;
     u32 slotw[kFrontWin];
   };
-  Board b2[kFrontP3Max];     // an item's ply-3 nodes' parents
+  union {
+    Board b2[kFrontP3Max];           // an item's ply-3 nodes' parents (selection)
+    uint16_t gw[4][kFrontBoardsMax]; // per-(group, board) word counts (from pass 1 on)
+  };
   Board b3[kFrontP3Max];     // an item's ply-3 nodes
   u32 r3[kFrontP3Max];       // ... their rank among the parent's moves
   uint16_t t3[kFrontP3Max];  // ... their tags (root move index)
   uint16_t m1[kFrontPly1Max];
-  u32 gc[4][kFrontPly1Max];  // per-group move counts (ply 2, selection, ply 4)
-  u32 noff[kFrontPly1Max];   // per-node move offsets (ply 2, ply 4)
-  u32 slot4[kFrontBoardsMax];         // E = 1: an item's ply-4 moves (ply-3 node << 12 | f | t << 6)
-  uint16_t wc[kFrontBoardsMax];       // per-board word counts
-  uint16_t gw[4][kFrontP3Max];        // per-(group, board) word counts (items of <= 64 boards)
-  u32 woff[kFrontBoardsMax];          // per-board word offsets
-  u64 red[4][3];
+  u32 gc[4][kFrontP3Max];    // per-group move counts (ply 2, selection, ply 4)
+  u32 noff[kFrontP3Max];     // per-node move offsets (ply 2, ply 4)
+  u32 slot4[kFrontBoardsMax];      // E = 1: an item's ply-4 moves (ply-3 node << 12 | f | t << 6)
+  u32 woff[kFrontBoardsMax];       // per-board word offsets
+  u64 red[kFrontWaves][3];
+  u64 tot[3];
   u32 g1[4];
-  u32 wsum[4];
+  u32 wsum[kFrontWaves];
   u32 jm;
 };
 
@@ -841,7 +850,7 @@ __device__ __forceinline__ u64 front_pack(u64 bad, u64 nb, u64 nw) {
 
 template <int S, class V>
 __device__ __forceinline__ void front_group_moves(u32 g, const Board& b, V&& visit) {
-  switch (g) {  // wave-uniform (g = wave index)
+  switch (g) {  // wave-uniform (g = wave % 4)
     case 0: ref_group_moves<S, 0>(b, visit); break;
     case 1: ref_group_moves<S, 1>(b, visit); break;
     case 2: ref_group_moves<S, 2>(b, visit); break;
@@ -858,73 +867,68 @@ __device__ __forceinline__ u32 front_group_count(u32 g, const Board& b) {
   }
 }
 
-// Sum of the (bad, boards, words) of every thread of the block.
+// Sum of the (bad, boards, words) of every thread of the block: per wave,
+// then the wave sums by wave 0.
 __device__ __forceinline__ void front_block_sum(FrontShared& sh, u64& bad, u64& nb, u64& nw) {
   bad = wave_sum64(bad);
   nb = wave_sum64(nb);
   nw = wave_sum64(nw);
-  const u32 w = threadIdx.x >> 6;
-  if (lane_id() == 0) {
+  const u32 w = threadIdx.x >> 6, l = lane_id();
+  if (l == 0) {
     sh.red[w][0] = bad;
     sh.red[w][1] = nb;
     sh.red[w][2] = nw;
   }
   __syncthreads();
-  bad = sh.red[0][0] + sh.red[1][0] + sh.red[2][0] + sh.red[3][0];
-  nb = sh.red[0][1] + sh.red[1][1] + sh.red[2][1] + sh.red[3][1];
-  nw = sh.red[0][2] + sh.red[1][2] + sh.red[2][2] + sh.red[3][2];
+  if (w == 0) {
+    const u64 x0 = wave_sum64(l < kFrontWaves ? sh.red[l][0] : 0ull);
+    const u64 x1 = wave_sum64(l < kFrontWaves ? sh.red[l][1] : 0ull);
+    const u64 x2 = wave_sum64(l < kFrontWaves ? sh.red[l][2] : 0ull);
+    if (l == 0) {
+      sh.tot[0] = x0;
+      sh.tot[1] = x1;
+      sh.tot[2] = x2;
+    }
+  }
   __syncthreads();
+  bad = sh.tot[0];
+  nb = sh.tot[1];
+  nw = sh.tot[2];
 }
 
 // Decoupled look-back: the (bad, boards, words) of items [0, it), read
-// backwards in windows of 1,024 items (4 per thread); a window holding an
+// backwards in windows of 1,024 items (one per thread); a window holding an
 // inclusive prefix ends the walk.  Every earlier item is held by a resident
 // block that takes its items in increasing order, so every slot waited on is
 // written.  The slots carry all the data exchanged, so the loads and stores
 // are relaxed device-scope atomics: acquire / release forms add a cache
 // invalidate or write-back per access (a spinning first version spent ~30 us
 // here).
-constexpr u32 kFrontLook = 4;
 __device__ __forceinline__ void front_lookback(FrontShared& sh, FrontState* st, u32 it, u64& bad, u64& nb, u64& nw) {
   const u32 t = threadIdx.x;
   bad = nb = nw = 0;
   u32 hi = it;
   while (hi > 0) {  // block-uniform
-    const u32 lo = hi > 256 * kFrontLook ? hi - 256 * kFrontLook : 0u;
-    u64 a[kFrontLook], inc[kFrontLook];
-#pragma unroll
-    for (u32 r = 0; r < kFrontLook; ++r) {
-      const u32 j = lo + r * 256 + t;
-      a[r] = inc[r] = 0;
-      if (j < hi) {
-        for (;;) {
-          a[r] = __hip_atomic_load(&st->agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (a[r] >> 63) break;
-          __builtin_amdgcn_s_sleep(2);  // (backoff: ~128 cycles between polls of a slot not yet written)
-        }
-        inc[r] = __hip_atomic_load(&st->incl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const u32 lo = hi > kFrontThreads ? hi - kFrontThreads : 0u;
+    const u32 j = lo + t;
+    u64 a = 0, inc = 0;
+    if (j < hi) {
+      for (;;) {
+        a = __hip_atomic_load(&st->agg[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (a >> 63) break;
+        __builtin_amdgcn_s_sleep(2);  // (backoff: ~128 cycles between polls of a slot not yet written)
       }
+      inc = __hip_atomic_load(&st->incl[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (t == 0) sh.jm = 0;
     __syncthreads();
-#pragma unroll
-    for (u32 r = 0; r < kFrontLook; ++r) {
-      const u32 j = lo + r * 256 + t;
-      if (j < hi && (inc[r] >> 63)) atomicMax(&sh.jm, j + 1);  // the window's last inclusive prefix (+1)
-    }
+    if (j < hi && (inc >> 63)) atomicMax(&sh.jm, j + 1);  // the window's last inclusive prefix (+1)
     __syncthreads();
     const u32 jm = sh.jm;  // 0: none in this window
-    u64 b1 = 0, n1 = 0, w1 = 0;
-#pragma unroll
-    for (u32 r = 0; r < kFrontLook; ++r) {
-      const u32 j = lo + r * 256 + t;
-      u64 v = 0;
-      if (jm && j == jm - 1) v = inc[r];
-      else if (j < hi && (!jm || j >= jm)) v = a[r];
-      b1 |= (v >> 62) & 1;
-      n1 += (v >> 40) & 0x3FFFFFull;
-      w1 += v & 0xFFFFFFFFFFull;
-    }
+    u64 v = 0;
+    if (jm && j == jm - 1) v = inc;
+    else if (j < hi && (!jm || j >= jm)) v = a;
+    u64 b1 = (v >> 62) & 1, n1 = (v >> 40) & 0x3FFFFFull, w1 = v & 0xFFFFFFFFFFull;
     front_block_sum(sh, b1, n1, w1);
     bad |= b1 ? 1ull : 0ull;
     nb += n1;
@@ -937,19 +941,27 @@ __device__ __forceinline__ void front_lookback(FrontShared& sh, FrontState* st, 
 // S0 = side to move at the root; E = plies between ply 3 and the boards written
 // (0: perft(6), boards = ply 3; 1: perft(7), boards = ply 4).  rng_out[0] = the
 // boards' Range, rng_out[1] = the words' (k_count3c's rng / rng_ch).
+// spill (kFrontSpillItems x kFrontWin words): an item of up to two windows
+// puts the words past the first in its spill row during the one walk and
+// copies them to their place after the look-back (a second walk of the item
+// made the ~3 % of startpos perft(7) items past one window the last blocks).
 template <int S0, int E>
-__global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p, u32 shard, u32 n_shards,
-                                               Board* __restrict__ out, uint16_t* __restrict__ out_tags, u32 cap_b,
-                                               u32* __restrict__ mw, u64 cap_w, PerftResult* __restrict__ res,
-                                               Range* __restrict__ rng_out, FrontState* __restrict__ st) {
+__global__ __launch_bounds__(kFrontThreads) void k_front(const Board* __restrict__ root_p, u32 shard, u32 n_shards,
+                                                         Board* __restrict__ out, uint16_t* __restrict__ out_tags,
+                                                         u32 cap_b, u32* __restrict__ mw, u64 cap_w,
+                                                         PerftResult* __restrict__ res, Range* __restrict__ rng_out,
+                                                         FrontState* __restrict__ st, u32* __restrict__ spill) {
   constexpr int S1 = S0 ^ 1;       // side to move at ply 1 (and ply 3)
   constexpr int SF = E ? S0 : S1;  // side to move at the boards written
+  constexpr u32 NT = kFrontThreads, NW = kFrontWaves;
   __shared__ FrontShared sh;
   const u32 t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const u32 grp = wave >> 2;                   // class group of the wave (waves 4g .. 4g + 3: one per SIMD)
+  const u32 qlane = lane + 64 * (wave & 3);    // the thread's index within its group (0 .. 255)
   DC_FRONT_STAMP(0);
   if (blockIdx.x == 0) {
     static_assert(sizeof(PerftResult) % 8 == 0, "PerftResult is cleared in u64 words");
-    for (u32 k = t; k < sizeof(PerftResult) / 8; k += 256) reinterpret_cast<u64*>(res)[k] = 0;
+    for (u32 k = t; k < sizeof(PerftResult) / 8; k += NT) reinterpret_cast<u64*>(res)[k] = 0;
   }
   const Board root = root_p[0];
   u32 n1 = 0, n2 = 0, n3 = 0;
@@ -957,12 +969,12 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
   // Returns false when it does not fit (block-uniform).  Block 0 records the
   // root moves (after the clear: barriers between).
   auto front_top = [&](bool record) -> bool {
-    // ply 1: wave g counts and walks class group g of the root
-    if (lane == 0) sh.g1[wave] = front_group_count<S0>(wave, root);
+    // ply 1: wave g < 4 counts and walks class group g of the root
+    if (wave < 4 && lane == 0) sh.g1[wave] = front_group_count<S0>(wave, root);
     __syncthreads();
     n1 = sh.g1[0] + sh.g1[1] + sh.g1[2] + sh.g1[3];
     if (n1 > kFrontPly1Max) return false;
-    if (lane == 0) {
+    if (wave < 4 && lane == 0) {
       u32 j = 0;
       for (u32 g = 0; g < wave; ++g) j += sh.g1[g];
       front_group_moves<S0>(wave, root, [&](int f, int to) { sh.m1[j++] = (uint16_t)(f | (to << 6)); });
@@ -977,26 +989,25 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     }
     __syncthreads();
     DC_FRONT_STAMP(1);
-    // ply 2: wave w takes class group w of nodes lane and 64 + lane
-    for (u32 node = lane; node < kFrontPly1Max; node += 64)
-      sh.gc[wave][node] = node < n1 ? front_group_count<S1>(wave, sh.top.p1[node]) : 0u;
+    // ply 2: group grp of node qlane
+    if (qlane < kFrontPly1Max) sh.gc[grp][qlane] = qlane < n1 ? front_group_count<S1>(grp, sh.top.p1[qlane]) : 0u;
     __syncthreads();
     const u32 tot = t < kFrontPly1Max ? sh.gc[0][t] + sh.gc[1][t] + sh.gc[2][t] + sh.gc[3][t] : 0u;
-    const u32 ex = block_excl_scan32<4>(tot, sh.wsum, &n2);
+    const u32 ex = block_excl_scan32<NW>(tot, sh.wsum, &n2);
     if (t < kFrontPly1Max) sh.noff[t] = ex;
     __syncthreads();
     DC_FRONT_STAMP(2);
     if (n2 > kFrontPly2Max) return false;
-    for (u32 node = lane; node < n1; node += 64) {
-      u32 j = sh.noff[node];
-      for (u32 g = 0; g < wave; ++g) j += sh.gc[g][node];
-      front_group_moves<S1>(wave, sh.top.p1[node],
-                            [&](int f, int to) { sh.top.w2[j++] = (node << 12) | (u32)f | ((u32)to << 6); });
+    if (qlane < n1) {
+      u32 j = sh.noff[qlane];
+      for (u32 g = 0; g < grp; ++g) j += sh.gc[g][qlane];
+      front_group_moves<S1>(grp, sh.top.p1[qlane],
+                            [&](int f, int to) { sh.top.w2[j++] = (qlane << 12) | (u32)f | ((u32)to << 6); });
     }
     __syncthreads();
     DC_FRONT_STAMP(3);
     // ply-3 counts of the ply-2 nodes, scanned in place into offsets
-    for (u32 j = t; j < n2; j += 256) {
+    for (u32 j = t; j < n2; j += NT) {
       const u32 e = sh.top.w2[j];
       Board b = sh.top.p1[e >> 12];
       ref_make(b, (int)(e & 63), (int)((e >> 6) & 63));
@@ -1004,10 +1015,10 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     }
     __syncthreads();
     DC_FRONT_STAMP(4);
-    const u32 seg = (n2 + 255) / 256, a = min(n2, t * seg), z = min(n2, a + seg);
+    const u32 seg = (n2 + NT - 1) / NT, a = min(n2, t * seg), z = min(n2, a + seg);
     u32 s = 0;
     for (u32 j = a; j < z; ++j) s += sh.top.off3[j];
-    u32 run = block_excl_scan32<4>(s, sh.wsum, &n3);
+    u32 run = block_excl_scan32<NW>(s, sh.wsum, &n3);
     for (u32 j = a; j < z; ++j) {
       const u32 v = sh.top.off3[j];
       sh.top.off3[j] = run;
@@ -1024,11 +1035,20 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     res->level_n[2] = n2;
     res->level_n[3] = n3;
   }
-  // ---- this rank's ply-3 nodes (shard, shard + n_shards, ...) in items of P3
+  // ---- this rank's ply-3 nodes (shard, shard + n_shards, ...): local index
+  //      k in [0, m3), cut into chunks of kFrontChunk consecutive nodes; item
+  //      i takes chunks i, i + n_items, i + 2 n_items, ... (one item per block
+  //      while its chunks fit kFrontP3Max).  Contiguous items of 35 nodes held
+  //      12k-32k words at perft(7), and the largest set the kernel's end.
+  //      (E = 0: one chunk per item -- contiguous items: their few words
+  //      vary little, and k_count3c's per-wave root tags stay uniform)
   const u32 m3 = ok && n3 > shard ? (n3 - shard + n_shards - 1) / n_shards : 0u;
-  u32 P3 = max(1u, (m3 + gridDim.x - 1) / gridDim.x);
-  P3 = min(kFrontP3Max, max(P3, (m3 + kFrontItemsMax - 1) / kFrontItemsMax));
-  const u32 n_items = (m3 + P3 - 1) / P3;
+  const u32 C = E ? kFrontChunk : min(kFrontP3Max, max(1u, (m3 + gridDim.x - 1) / gridDim.x));
+  const u32 NC = (m3 + C - 1) / C;
+  u32 n_items = min(gridDim.x, NC);
+  n_items = max(n_items, (NC + kFrontP3Max / C - 1) / (kFrontP3Max / C));
+  n_items = min(n_items, kFrontItemsMax);  // (more chunks than that per item: declined below)
+  const u32 cpi = n_items ? (NC + n_items - 1) / n_items : 0u;  // chunks per item
   if (blockIdx.x == 0 && t == 0) st->n_items = n_items;  // (k_count3c clears that many slots)
   if (!ok || n_items == 0) {  // nothing to expand: block 0 publishes the result
     if (blockIdx.x == 0 && t == 0) {
@@ -1043,11 +1063,17 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
   }
   for (u32 it = blockIdx.x; it < n_items; it += gridDim.x) {
     if (it != blockIdx.x) (void)front_top(false);  // the previous item's words overwrote it
-    const u32 k0 = it * P3, np3 = min(P3, m3 - k0);
-    // -- select the item's ply-3 nodes: parent by binary search (wave 0), the
-    //    rank's class group by one group count per wave, the move by one walk
-    if (wave == 0 && lane < np3) {
-      const u32 q = shard + (k0 + lane) * n_shards;
+    // the item's nodes: lane t -> chunk it + n_items (t / C), node t % C in
+    // it; the valid lanes are a prefix (only chunk NC - 1 can be short)
+    const u32 cj = it < NC ? (NC - 1 - it) / n_items + 1 : 0u;  // chunks of this item
+    const u32 last_c = it + n_items * (cj - 1);
+    const u32 np3 = cpi * C > kFrontP3Max ? 0u : (cj - 1) * C + min(C, m3 - last_c * C);
+    const bool too_big = cpi * C > kFrontP3Max;  // block-uniform (flagged below)
+    // -- select the item's ply-3 nodes: parent by binary search, the rank's
+    //    class group by one group count per (node, group), the move by one walk
+    if (t < np3) {
+      const u32 k = (it + n_items * (t / C)) * C + t % C;
+      const u32 q = shard + k * n_shards;
       u32 lo = 0, hi = n2;  // the last ply-2 node whose offset is <= q (it has q's move)
       while (hi - lo > 1) {
         const u32 mid = (lo + hi) >> 1;
@@ -1057,21 +1083,21 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
       const u32 e = sh.top.w2[lo];
       Board b2 = sh.top.p1[e >> 12];
       ref_make(b2, (int)(e & 63), (int)((e >> 6) & 63));
-      sh.b2[lane] = b2;
-      sh.r3[lane] = q - sh.top.off3[lo];
-      sh.t3[lane] = (uint16_t)(e >> 12);
+      sh.b2[t] = b2;
+      sh.r3[t] = q - sh.top.off3[lo];
+      sh.t3[t] = (uint16_t)(e >> 12);
     }
     __syncthreads();
-    if (lane < np3) sh.gc[wave][lane] = front_group_count<S0>(wave, sh.b2[lane]);
+    if (qlane < np3) sh.gc[grp][qlane] = front_group_count<S0>(grp, sh.b2[qlane]);
     __syncthreads();
-    if (lane < np3) {
-      u32 r = sh.r3[lane];
-      for (u32 g = 0; g < wave; ++g) r -= sh.gc[g][lane];  // (wraps when the move is in an earlier group)
-      if (r < sh.gc[wave][lane]) {
+    if (qlane < np3) {
+      u32 r = sh.r3[qlane];
+      for (u32 g = 0; g < grp; ++g) r -= sh.gc[g][qlane];  // (wraps when the move is in an earlier group)
+      if (r < sh.gc[grp][qlane]) {
         int f = 0, to = 0;
         u32 k = 0;
-        const Board b2 = sh.b2[lane];
-        front_group_moves<S0>(wave, b2, [&](int ff, int tt) {
+        const Board b2 = sh.b2[qlane];
+        front_group_moves<S0>(grp, b2, [&](int ff, int tt) {
           if (k == r) {
             f = ff;
             to = tt;
@@ -1080,27 +1106,27 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
         });
         Board b3 = b2;
         ref_make(b3, f, to);
-        sh.b3[lane] = b3;
+        sh.b3[qlane] = b3;
       }
     }
     __syncthreads();
     if (it == blockIdx.x) DC_FRONT_STAMP(6);
     // -- the item's boards: E = 0 the ply-3 nodes, E = 1 their children
     u32 nbd = np3;
-    bool bad = false;
+    bool bad = too_big;
     if constexpr (E == 1) {
-      if (lane < np3) sh.gc[wave][lane] = front_group_count<S1>(wave, sh.b3[lane]);
+      if (qlane < np3) sh.gc[grp][qlane] = front_group_count<S1>(grp, sh.b3[qlane]);
       __syncthreads();
       const u32 tot = t < np3 ? sh.gc[0][t] + sh.gc[1][t] + sh.gc[2][t] + sh.gc[3][t] : 0u;
-      const u32 ex = block_excl_scan32<4>(tot, sh.wsum, &nbd);
-      if (t < 64) sh.noff[t] = ex;
+      const u32 ex = block_excl_scan32<NW>(tot, sh.wsum, &nbd);
+      if (t < kFrontP3Max) sh.noff[t] = ex;
       __syncthreads();
       bad = nbd > kFrontBoardsMax;  // block-uniform
-      if (!bad && lane < np3) {
-        u32 j = sh.noff[lane];
-        for (u32 g = 0; g < wave; ++g) j += sh.gc[g][lane];
-        front_group_moves<S1>(wave, sh.b3[lane],
-                              [&](int f, int to) { sh.slot4[j++] = (lane << 12) | (u32)f | ((u32)to << 6); });
+      if (!bad && qlane < np3) {
+        u32 j = sh.noff[qlane];
+        for (u32 g = 0; g < grp; ++g) j += sh.gc[g][qlane];
+        front_group_moves<S1>(grp, sh.b3[qlane],
+                              [&](int f, int to) { sh.slot4[j++] = (qlane << 12) | (u32)f | ((u32)to << 6); });
       }
       __syncthreads();
       if (it == blockIdx.x) DC_FRONT_STAMP(7);
@@ -1116,26 +1142,18 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
         return sh.b3[k];
       }
     };
-    // -- pass 1: word counts.  Up to 64 boards: per (group, board), wave g
-    //    taking group g (a lane walks a quarter of a board later); more: per
-    //    board, boards dealt round-robin over the waves (k % 4 = wave).
-    const bool split = nbd <= kFrontP3Max;  // block-uniform
-    if (split) {
-      if (lane < nbd) sh.gw[wave][lane] = (uint16_t)front_group_count<SF>(wave, board_at(lane));
-      __syncthreads();
-      if (t < nbd) sh.wc[t] = (uint16_t)(sh.gw[0][t] + sh.gw[1][t] + sh.gw[2][t] + sh.gw[3][t]);
-    } else {
-      for (u32 k = wave + 4 * lane; k < nbd; k += 256) sh.wc[k] = (uint16_t)ref_count<SF>(board_at(k));
-    }
+    // -- pass 1: word counts per (group, board)
+    for (u32 k = qlane; k < nbd; k += 256) sh.gw[grp][k] = (uint16_t)front_group_count<SF>(grp, board_at(k));
     __syncthreads();
-    const u32 seg = (nbd + 255) / 256, a = min(nbd, t * seg), z = min(nbd, a + seg);
+    const u32 seg = (nbd + NT - 1) / NT, a = min(nbd, t * seg), z = min(nbd, a + seg);
+    auto wcount = [&](u32 k) -> u32 { return (u32)sh.gw[0][k] + sh.gw[1][k] + sh.gw[2][k] + sh.gw[3][k]; };
     u32 s = 0;
-    for (u32 k = a; k < z; ++k) s += sh.wc[k];
+    for (u32 k = a; k < z; ++k) s += wcount(k);
     u32 nw;
-    u32 run = block_excl_scan32<4>(s, sh.wsum, &nw);
+    u32 run = block_excl_scan32<NW>(s, sh.wsum, &nw);
     for (u32 k = a; k < z; ++k) {
       sh.woff[k] = run;
-      run += sh.wc[k];
+      run += wcount(k);
     }
     // -- publish the item's counts, walk its words into the first LDS window
     //    (board index relative to the item, rebased when stored), then look
@@ -1146,28 +1164,22 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     if (it == blockIdx.x) DC_FRONT_STAMP(12);
 #endif
     __syncthreads();  // woff / wc
-    auto walk = [&](u32 wb) {  // the words [wb, wb + kFrontWin) into slotw
-      if (split) {
-        if (lane < nbd) {
-          u32 j = sh.woff[lane];
-          for (u32 g = 0; g < wave; ++g) j += sh.gw[g][lane];
-          const u32 c = sh.gw[wave][lane];
-          if (c && j < wb + kFrontWin && j + c > wb)
-            front_group_moves<SF>(wave, board_at(lane), [&](int f, int to) {
-              if (j >= wb && j - wb < kFrontWin) sh.slotw[j - wb] = (lane << 12) | (u32)f | ((u32)to << 6);
-              ++j;
-            });
-        }
-      } else {
-        for (u32 k = wave + 4 * lane; k < nbd; k += 256) {
-          u32 j = sh.woff[k];
-          const u32 c = sh.wc[k];
-          if (c && j < wb + kFrontWin && j + c > wb)
-            ref_for_each_move<SF>(board_at(k), [&](int f, int to) {
-              if (j >= wb && j - wb < kFrontWin) sh.slotw[j - wb] = (k << 12) | (u32)f | ((u32)to << 6);
-              ++j;
-            });
-        }
+    // the words [wb, wb + kFrontWin) into slotw; the first walk also puts
+    // [kFrontWin, 2 kFrontWin) into the item's spill row when it has one
+    u32* srow = spill && it < kFrontSpillItems && nw <= 2 * kFrontWin ? spill + (size_t)it * kFrontWin : nullptr;
+    auto walk = [&](u32 wb) {
+      const u32 we = wb + (wb == 0 && srow ? 2 * kFrontWin : kFrontWin);
+      for (u32 k = qlane; k < nbd; k += 256) {
+        u32 j = sh.woff[k];
+        for (u32 g = 0; g < grp; ++g) j += sh.gw[g][k];
+        const u32 c = sh.gw[grp][k];
+        if (c && j < we && j + c > wb)
+          front_group_moves<SF>(grp, board_at(k), [&](int f, int to) {
+            const u32 w = (k << 12) | (u32)f | ((u32)to << 6);
+            if (j >= wb && j - wb < kFrontWin) sh.slotw[j - wb] = w;
+            else if (j >= wb + kFrontWin && j < we) srow[j - wb - kFrontWin] = w;
+            ++j;
+          });
       }
       __syncthreads();
     };
@@ -1185,7 +1197,7 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
     const bool fits = !pbad && !bad && base_b + nbd <= cap_b;  // (else flagged below: no store)
     // -- the boards, then the words window by window
     if (fits)
-      for (u32 k = t; k < nbd; k += 256) {
+      for (u32 k = t; k < nbd; k += NT) {
         store_board(out, base_b + k, board_at(k));
         out_tags[base_b + k] = E == 1 ? sh.t3[sh.slot4[k] >> 12] : sh.t3[k];
       }
@@ -1198,12 +1210,19 @@ __global__ __launch_bounds__(256) void k_front(const Board* __restrict__ root_p,
 #endif
     const u32 rebase = (u32)base_b << 12;
     for (u32 wb = 0; fits && wb < nw; wb += kFrontWin) {  // block-uniform
+      const u32 ns = min(kFrontWin, nw - wb);
+      if (wb && srow) {  // the spilled second window (written by this block's walk)
+        for (u32 r = t; r < ns; r += NT) {
+          const u64 o = base_w + wb + r;
+          if (o < cap_w) mw[o] = srow[r] + rebase;
+        }
+        continue;
+      }
       if (wb) {
         __syncthreads();  // the previous window is stored
         walk(wb);
       }
-      const u32 ns = min(kFrontWin, nw - wb);
-      for (u32 r = t; r < ns; r += 256) {
+      for (u32 r = t; r < ns; r += NT) {
         const u64 o = base_w + wb + r;
         if (o < cap_w) mw[o] = sh.slotw[r] + rebase;
       }
@@ -2794,16 +2813,19 @@ extern "C" __attribute__((visibility("default"))) int dc_ab_front_trace(u64* out
 }
 #endif
 
+u64 front_spill_words() { return (u64)kFrontSpillItems * kFrontWin; }
+
 hipError_t launch_front(hipStream_t st, int stm0, u32 depth, const Board* root, u32 shard, u32 n_shards, Board* out,
                         uint16_t* out_tags, u32 cap_b, u32* mw, u64 cap_w, PerftResult* res, Range* rng_out,
-                        FrontState* fst) {
+                        FrontState* fst, u32* spill) {
   if (depth != 6 && depth != 7) return hipErrorInvalidValue;
   // one pass of the resident grid: every block does the top once
 #define DC_FRONT(S, E)                                                                                        \
   do {                                                                                                        \
     auto k_ = k_front<S, E>;                                                                                  \
-    hipLaunchKernelGGL(k_, dim3(resident_grid(k_, 256, kMaxGrid)), dim3(256), 0, st, root, shard, n_shards, \
-                       out, out_tags, cap_b, mw, cap_w, res, rng_out, fst);                                   \
+    hipLaunchKernelGGL(k_, dim3(resident_grid(k_, kFrontThreads, kMaxGrid)), dim3(kFrontThreads), 0, st, root,    \
+                       shard, n_shards,                                                                       \
+                       out, out_tags, cap_b, mw, cap_w, res, rng_out, fst, spill);                            \
   } while (0)
   if (depth == 7) {
     if (stm0) DC_FRONT(1, 1);

@@ -138,11 +138,14 @@ def test_fide_validate_replay_live_beside_single_issue_waves(engine, noise, kind
         rng = np.random.default_rng(kind)
         idx = [rng.choice(len(mvs), 1 + int(rng.integers(0, 64)), replace=False) for _ in range(150)]
         want_l = [live.validate_batch(pos[i], mvs[i], rules=F) for i in idx]
+        # the live calls first: their wave is resident from before the noise
+        # (the engine's calls below stop it, LiveHold, and a relaunch would
+        # queue behind the noise blocks)
         with noise(kind, 4000):
+            got_l = [live.validate_batch(pos[i], mvs[i], rules=F) for i in idx]
             got_v = [engine.validate_batch(pos, mvs, rules=F) for _ in range(2)]
             got_g = engine.gen_games(919, 0, 1 << 16, 80, 32, rules=F)
             got_r = engine.replay(got_g, rules=F)
-            got_l = [live.validate_batch(pos[i], mvs[i], rules=F) for i in idx]
     finally:
         live.live_validator(0)
         live.close()

@@ -6,7 +6,7 @@ ply-3 scan, the item's ply-3 nodes selected, its ply-4 moves enumerated (depth
 clock read by thread 0 after each barrier).  Printed: the median over blocks
 of each stamp, and percentiles of entry and done times over all blocks, by
 block-index quartile.
-GPU tool: DCHESS_LIB=.../libdchess_ab.so python tools/front_trace.py [depth]"""
+GPU tool: DCHESS_LIB=.../libdchess_ab.so python tools/front_trace.py [depth] [shards]"""
 import ctypes
 import json
 import os
@@ -20,6 +20,7 @@ import dchess  # noqa: E402
 
 NB, NW = 2048, 16
 depth = int(sys.argv[1]) if len(sys.argv) > 1 else 7
+shards = int(sys.argv[2]) if len(sys.argv) > 2 else 1  # shard 0 of N (one rank's work at N GPUs)
 eng = dchess.Engine(0)
 lib = ctypes.CDLL(os.environ["DCHESS_LIB"])
 lib.dc_ab_front_trace.argtypes = [ctypes.c_void_p]
@@ -30,7 +31,10 @@ runs = []
 for _ in range(6):
     buf[:] = 0
     assert lib.dc_ab_front_trace(buf.ctypes.data) == 0  # (clears nothing: read the previous run's, then rerun)
-    eng.perft(dchess.startpos(), depth)
+    if shards > 1:
+        eng.perft_shard(dchess.startpos(), depth, 3, 0, shards)
+    else:
+        eng.perft(dchess.startpos(), depth)
     assert lib.dc_ab_front_trace(buf.ctypes.data) == 0
     t = buf.astype(np.int64).reshape(NB, NW)
     used = t[:, 0] > 0
@@ -55,4 +59,4 @@ for _ in range(6):
                            for i in slow]
 out = {k: round(float(np.median([r[k] for r in runs[1:]])), 2) for k in runs[0] if k != "slowest"}
 out["slowest_last_run(block,publish,boards,words,select,scan)"] = runs[-1]["slowest"]
-print(json.dumps({"depth": depth, "stamps_us": out}))
+print(json.dumps({"depth": depth, "shards": shards, "stamps_us": out}))
