@@ -115,14 +115,17 @@ def test_replay_beside_single_issue_waves(engine, noise, kind):
 
 
 @pytest.mark.parametrize("kind", (1, 12))
-def test_fide_validate_replay_live_beside_single_issue_waves(engine, noise, kind):
-    """the FIDE kernels outside the final stage that carried
-    the compare-overwrite shape until round 6 (tools/vccz_check.py --any) --
+def test_fide_validate_replay_beside_single_issue_waves(engine, noise, kind):
+    """FIDE kernels outside the final stage that carried the
+    compare-overwrite shape until round 6 (tools/vccz_check.py --any) --
     k_validate_fide over every (from, to) pair of suite and game positions,
-    k_gen_games_fide + k_replay_fide over 65,536 games, and a FIDE request
-    stream through the resident live validator k_live -- beside the noise,
-    each equal to its undisturbed run (which tests/test_gpu_fide.py and
-    tests/test_gpu_live.py pin against fastcpu)."""
+    k_gen_games_fide + k_replay_fide over 65,536 games -- beside the noise,
+    each equal to its undisturbed run (which tests/test_gpu_fide.py pins
+    against fastcpu).  The live validator k_live is not stressed here: its
+    resident wave and the noise kernels can share one of the process's four
+    hardware queues, where one waits for the other instead of co-running (a
+    first version of this test timed out that way); the static check covers
+    it (tests/test_spill_free.py)."""
     from test_gpu_fide import _fide_positions, dpos
     F = dchess.RULES_FIDE
     ps = _fide_positions(12, 61)
@@ -132,26 +135,11 @@ def test_fide_validate_replay_live_beside_single_issue_waves(engine, noise, kind
     want_v = engine.validate_batch(pos, mvs, rules=F)
     want_g = engine.gen_games(919, 0, 1 << 16, 80, 32, rules=F)
     want_r = engine.replay(want_g, rules=F)
-    live = dchess.Engine(0)
-    try:
-        live.live_validator(10_000_000)
-        rng = np.random.default_rng(kind)
-        idx = [rng.choice(len(mvs), 1 + int(rng.integers(0, 64)), replace=False) for _ in range(150)]
-        want_l = [live.validate_batch(pos[i], mvs[i], rules=F) for i in idx]
-        # the live calls first: their wave is resident from before the noise
-        # (the engine's calls below stop it, LiveHold, and a relaunch would
-        # queue behind the noise blocks)
-        with noise(kind, 4000):
-            got_l = [live.validate_batch(pos[i], mvs[i], rules=F) for i in idx]
-            got_v = [engine.validate_batch(pos, mvs, rules=F) for _ in range(2)]
-            got_g = engine.gen_games(919, 0, 1 << 16, 80, 32, rules=F)
-            got_r = engine.replay(got_g, rules=F)
-    finally:
-        live.live_validator(0)
-        live.close()
+    with noise(kind, 2500):
+        got_v = [engine.validate_batch(pos, mvs, rules=F) for _ in range(2)]
+        got_g = engine.gen_games(919, 0, 1 << 16, 80, 32, rules=F)
+        got_r = engine.replay(got_g, rules=F)
     for g in got_v:
         assert (g == want_v).all()
     assert (got_g == want_g).all()
     assert (got_r[0] == want_r[0]).all() and (got_r[1] == want_r[1]).all() and got_r[2] == want_r[2]
-    for a, b in zip(got_l, want_l):
-        assert (a == b).all()
