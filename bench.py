@@ -229,16 +229,17 @@ def perft_contexts(eng, d, n):
 
 def perft_streams(args, depth, world=1):
     """Contexts a repeated perft(depth) is spread over.  One perft's front end
-    (the one-workgroup top expansion and the level chain before the final stage,
-    ~70 us) is latency-bound; with the steps split over two or three contexts --
+    (round 6: one k_front launch, ~45 us at perft(7), ~22 us at perft(6)) does
+    not fill the GPU; with the steps split over two or three contexts --
     streams -- one run's front end executes while another's final stage holds
-    the CUs (tools/overlap_perft.py, profiles/r05/overlap_u.jsonl: perft(7)
-    0.408 -> 0.378 ms per step with 2, perft(6) 0.068 -> 0.034 with 3).  A rank
-    of N >= 4 holds a shard whose final stage is shorter than the front end, so
-    perft(7) takes 3 there (shard 0 of 8: 0.116 ms on one context, 0.070 on
-    two, 0.062 on three; profiles/r05/overlap_ab_shards.jsonl).  Every step is
-    still a whole perft (of this rank's shard) with its own result record.  Deep
-    runs (the final stage is everything) keep one."""
+    the CUs (tools/overlap_perft.py, profiles/r06/overlap_ctx.jsonl, overlap_q:
+    perft(7) 0.376 -> 0.351 ms per step with 2, 0.353 with 3; perft(6) 0.048 ->
+    0.036 with 2 or 3).  A rank of N >= 4 holds a shard whose final stage is
+    about as long as its front end, so perft(7) takes 3 there (shard 0 of 8:
+    0.085 ms on one context, 0.064 on two).  Every step is still a whole perft
+    (of this rank's shard) with its own result record; the bench line also
+    reports the one-context figures (perft_one_stream).  Deep runs (the final
+    stage is everything) keep one."""
     if args.perft_streams:
         return args.perft_streams
     return 3 if depth <= 6 else (3 if world >= 4 else 2) if depth == 7 else 1
