@@ -1489,6 +1489,9 @@ extern "C" __attribute__((visibility("default"))) int dc_diag_child_set(void* de
 #ifndef DC_C2B_DYN
 #define DC_C2B_DYN 1
 #endif
+#ifndef DC_C2B_EVEN
+#define DC_C2B_EVEN 0
+#endif
 template <class R, int STM>
 __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
@@ -1511,7 +1514,15 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
   // for mid-size levels measured slower on the suite batch: 0.426 vs 0.418 ms,
   // profiles/r05/ab_z2.jsonl.)
   const u64 share = max<u64>(1, (hi - lo + gridDim.x - 1) / gridDim.x);
+#if DC_C2B_EVEN
+  // DC_C2B_EVEN (round 6 A/B): a level of r < share / 256 <= r + 1 rounds of
+  // full chunks (the suite batch: 1.22 rounds, 938 chunks over 768 blocks)
+  // in ceil(share / 256) rounds of equal chunks instead.  Measured slower
+  // (profiles/r06/ab_c2b_even.txt): the suite's final stage 0.355 -> 0.366 ms.
+  const u64 cs = (share + (share + kChunk - 1) / kChunk - 1) / ((share + kChunk - 1) / kChunk);
+#else
   const u64 cs = min<u64>(kChunk, share);
+#endif
   const u64 nch = (hi - lo + cs - 1) / cs;
   for (u64 c = blockIdx.x; c < nch;) {  // block-uniform
     const u64 s = lo + c * cs;
@@ -2282,6 +2293,9 @@ __global__ __launch_bounds__(256, MINW) void k_count2c(const Board* __restrict__
 // per grandparent enumerating into LDS while the block waited -- made the
 // final stage 0.56 vs 0.49 + 0.04 ms.)
 constexpr u32 kGroup = 256;
+#ifndef DC_C3C_EVEN
+#define DC_C3C_EVEN 0
+#endif
 #ifndef DC_C3C_LOG
 #define DC_C3C_LOG 0
 #endif
@@ -2323,15 +2337,31 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
   // Each block's first group is its own index (round 5: no atomic round trip
   // before the first load, as in k_count2b); the counter hands out the rest
   // from gridDim.x on.
+#if DC_C3C_EVEN
+  // DC_C3C_EVEN (round 6): groups of gsz <= 256 words, gsz chosen so that the
+  // level is a whole number of rounds of the grid.  With 256-word groups a
+  // strided shard of perft(7) (613k words: 2.34 rounds of 1,024 blocks) ran
+  // its last third of a round on a third of the blocks, one group's latency
+  // at low occupancy: its k_count3c took 57 us for 41 us of work.  Measured
+  // slower (profiles/r06/ab_c3even.jsonl, same box, alternating): shard 0 of 8
+  // 0.084 -> 0.091 ms, perft(6) 0.047 -> 0.049 ms, perft(7) unchanged: more
+  // groups means more per-group parent splits, whose issue cost does not
+  // shrink with the group.  Off (A/B knob).
+  const u32 rounds = (total + kGroup * gridDim.x - 1) / (kGroup * gridDim.x);
+  const u32 gsz = rounds ? (total + rounds * gridDim.x - 1) / (rounds * gridDim.x) : kGroup;
+#else
+  constexpr u32 gsz = kGroup;
+#endif
   u32 grp = blockIdx.x;
   for (;;) {
     // (fetching the next group's index one group ahead, to take its round
     // trip off the load chain, made the kernel 0.495 -> 0.519 ms at perft(7):
     // a block then holds a group it cannot start, which lengthens the tail)
-    const u64 s = (u64)grp * kGroup;
+    const u64 s = (u64)grp * gsz;
     if (s >= total) break;  // block-uniform
-    const u64 i = s + otid(wave);
-    const bool valid = i < total;
+    const u32 ot = otid(wave);
+    const u64 i = s + ot;
+    const bool valid = ot < gsz && i < total;
     Board ch{0, 0, 0, 0};
     u32 tag = 0;
     if (valid) {

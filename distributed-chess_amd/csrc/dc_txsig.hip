@@ -48,9 +48,26 @@ __global__ __launch_bounds__(kTxThreads, DC_TX_MINW) void k_verify_tx(const char
   const u32 o0 = off[b], o1 = off[b + 1], o2 = off[b + 2], o3 = off[b + 3], o4 = off[b + 4];
   const u32 act[4] = {actions[b], actions[b + 1], actions[b + 2], actions[b + 3]};
   const int turn = turns ? (int)turns[i] : -1;
-  verdicts[i] = (uint8_t)secp::check_tx(strings + o0, o1 - o0, strings + o1, o2 - o1, act, strings + o2, o3 - o2,
-                                        strings + o3, o4 - o3, turn, gtab,
-                                        secp::BlkRef{&blk[0][threadIdx.x][0], kTxThreads * 4});
+  // The owner comparison (is_valid_tx, hotstuff.rs:141-148) is made here,
+  // before the message hash, and applied after check_tx (which then skips
+  // it): check_tx made it after the ~2.7k-multiplication verify, by which time
+  // the key's and the name's lines had left the caches, so both strings were
+  // fetched from HBM twice.  A bad signature still outranks a wrong owner.
+  // The bit waits in LDS (a VGPR live across the verify spills at the 248-VGPR
+  // budget).
+  __shared__ uint8_t own_bit[kTxThreads];
+  {
+    const char* pk = strings + o3;
+    const u32 pl = o4 - o3;
+    own_bit[threadIdx.x] =
+        turn < 0 ? 1 : (turn == 0 ? secp::str_eq(pk, pl, strings + o0, o1 - o0) : secp::str_eq(pk, pl, strings + o1, o2 - o1));
+  }
+  int skip = -1;  // check_tx's own owner branch, kept but never taken: with a
+  asm volatile("" : "+v"(skip));  // constant -1 folded in, its body spilled 344 B
+  u32 v = secp::check_tx(strings + o0, o1 - o0, strings + o1, o2 - o1, act, strings + o2, o3 - o2, strings + o3, o4 - o3,
+                         skip, gtab, secp::BlkRef{&blk[0][threadIdx.x][0], kTxThreads * 4});
+  if (v == secp::SIG_OK && !*(volatile uint8_t*)&own_bit[threadIdx.x]) v = secp::SIG_WRONG_OWNER;
+  verdicts[i] = (uint8_t)v;
 }
 
 hipError_t launch_secp_gtab(hipStream_t st, secp::Ge* gtab) {
