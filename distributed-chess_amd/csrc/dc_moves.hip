@@ -755,15 +755,38 @@ __device__ __forceinline__ void gen_tabs_build(GenTabs& T) {
   }
 }
 
+// DC_GEN_LDS1 (round 6): every table read is its own ds_read_b64.  Reads of
+// two rows at one square (NE and NW, N and E) sit 512 B apart, so the
+// compiler merged them into ds_read2st64_b64, which serves a wave in 16-lane
+// groups banked (a/4) mod 32: squares s and s + 16k of one group collide, and
+// per-lane squares are random.  ds_read_b64 serves 32-lane groups banked
+// (a/4) mod 64 (only s and s + 32 collide) at 2 LDS cycles against 8: the
+// kernel had 2.10 conflict cycles per LDS cycle.  The row index goes through
+// an empty asm so no two reads share a base register.  Measured (same box,
+// alternating, profiles/r06/ab_gen_lds1.txt): conflicts 2.10 -> 0.74 per LDS
+// cycle and wait fraction 0.67 -> 0.63, but 41 LDS reads per ply slot instead
+// of 29 and 4.7 % more VALU (the addresses), and the kernel 18.27 -> 18.57 ms:
+// the conflicts were not what it waits on.  Off (A/B knob).
+#ifndef DC_GEN_LDS1
+#define DC_GEN_LDS1 0
+#endif
+template <int D>
+__device__ __forceinline__ u64 gen_tab_ray(const GenTabs& T, int s) {
+#if DC_GEN_LDS1
+  asm volatile("" : "+v"(s));
+#endif
+  return T.ray[D][s];
+}
+
 // Ray of direction D from s up to and including the first occupied square:
 // the table ray minus the ray beyond that blocker (a sentinel blocker on the
 // edge square whose ray is empty makes the unblocked case the same formula).
 template <int D>
 __device__ __forceinline__ u64 gen_ray(const GenTabs& T, int s, u64 occ) {
-  const u64 r = T.ray[D][s];
+  const u64 r = gen_tab_ray<D>(T, s);
   const u64 bl = r & occ;
   const int b = (D & 1) == 0 ? lsb(bl | (1ull << 63)) : msb(bl | 1ull);
-  return r ^ T.ray[D][b];
+  return r ^ gen_tab_ray<D>(T, b);
 }
 
 // Ray of a direction D that runs to higher squares (N, E, NE, NW) up to and
@@ -774,7 +797,7 @@ __device__ __forceinline__ u64 gen_ray(const GenTabs& T, int s, u64 occ) {
 template <int D>
 __device__ __forceinline__ u64 gen_ray_up(const GenTabs& T, int s, u64 occ) {
   static_assert(D == 0 || D == 2 || D == 4 || D == 6, "a direction to higher squares");
-  const u64 r = T.ray[D][s];
+  const u64 r = gen_tab_ray<D>(T, s);
   const u64 bl = r & occ;
   return r & (bl ^ (bl - 1));
 }
@@ -794,6 +817,26 @@ __device__ __forceinline__ u64 gen_ray_up(const GenTabs& T, int s, u64 occ) {
 // slots -- 8 slots for the binary search to sum instead of 9 (2 B + Q, 2 R + Q).
 #ifndef DC_GEN_QSLOT
 #define DC_GEN_QSLOT 1
+#endif
+// DC_GEN_NOBR (round 6 A/B): the slider slots' ray reads without the per-slot
+// wave-uniform skip (an empty slot reads square 0 and its count is masked).
+// DC_GEN_BATCH (round 6 A/B): every table read of a ply (27 for the slot
+// counts, 11 for the chosen piece) issued ahead of its use, held there by
+// empty asms.  The kernel waits 0.67 of its wave cycles, with one
+// lgkmcnt(0) after nearly every read, so the reads looked like the bound.
+// Measured (profiles/r06/ab_gen_batch.txt, same box, alternating): 18.20 ->
+// 19.29 ms.  The held reads take 117-122 VGPRs (4 waves/SIMD instead of 6),
+// and with more reads in flight per wave the conflicts rose from 2.10 to
+// 3.58 per LDS cycle: the waits were overlapped by other waves' issue all
+// along.  Both off.
+#ifndef DC_GEN_NOBR
+#define DC_GEN_NOBR 0
+#endif
+#ifndef DC_GEN_BATCH
+#define DC_GEN_BATCH 0
+#endif
+#if DC_GEN_BATCH && !(DC_GEN_POSRAY && DC_GEN_QSLOT)
+#error "DC_GEN_BATCH needs DC_GEN_POSRAY and DC_GEN_QSLOT"
 #endif
 constexpr int kGenLine = DC_GEN_QSLOT ? 2 : 3;  // slots per slider line kind
 constexpr int kGenSlots = 3 + 2 * kGenLine + (DC_GEN_QSLOT ? 1 : 0);
@@ -832,6 +875,59 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
       rem &= rem - 1;
       return any;
     };
+#if DC_GEN_BATCH
+    {
+      // every slot's square first (view squares; 0 for an empty slot), then
+      // every table read, then the counts: the reads issue together and
+      // their latency overlaps (the slot-by-slot form waited on each read)
+      u64 rem = sw.N;
+      int n0, n1, k0, b0, b1, r0, r1, q0;
+      const bool an0 = take(rem, n0), an1 = take(rem, n1);
+      rem = sw.K;
+      const bool ak = take(rem, k0);
+      rem = sw.D & ~sw.O;
+      const bool ab0 = take(rem, b0), ab1 = take(rem, b1);
+      rem = sw.O & ~sw.D;
+      const bool ar0 = take(rem, r0), ar1 = take(rem, r1);
+      rem = sw.D & sw.O;
+      const bool aq = take(rem, q0);
+      u64 tn0 = T.kn[n0], tn1 = T.kn[n1], tk = T.kg[k0];
+      u64 b0ne = T.ray[4][b0], b0nw = T.ray[6][b0], b0se = T.ray[4][b0 ^ 56], b0sw = T.ray[6][b0 ^ 56];
+      u64 b1ne = T.ray[4][b1], b1nw = T.ray[6][b1], b1se = T.ray[4][b1 ^ 56], b1sw = T.ray[6][b1 ^ 56];
+      u64 r0n = T.ray[0][r0], r0e = T.ray[2][r0], r0w = T.ray[3][r0], r0s = T.ray[0][r0 ^ 56];
+      u64 r1n = T.ray[0][r1], r1e = T.ray[2][r1], r1w = T.ray[3][r1], r1s = T.ray[0][r1 ^ 56];
+      u64 qn = T.ray[0][q0], qe = T.ray[2][q0], qw = T.ray[3][q0], qne = T.ray[4][q0], qnw = T.ray[6][q0];
+      u64 qs = T.ray[0][q0 ^ 56], qse = T.ray[4][q0 ^ 56], qsw = T.ray[6][q0 ^ 56];
+      // (the empty asms hold the reads ahead of the counts: the scheduler
+      // otherwise sinks each read to its use, one wait per read)
+      asm volatile("" : "+v"(tn0), "+v"(tn1), "+v"(tk), "+v"(b0ne), "+v"(b0nw), "+v"(b0se), "+v"(b0sw));
+      asm volatile("" : "+v"(b1ne), "+v"(b1nw), "+v"(b1se), "+v"(b1sw), "+v"(r0n), "+v"(r0e), "+v"(r0w), "+v"(r0s));
+      asm volatile("" : "+v"(r1n), "+v"(r1e), "+v"(r1w), "+v"(r1s), "+v"(qn), "+v"(qe), "+v"(qw), "+v"(qne));
+      asm volatile("" : "+v"(qnw), "+v"(qs), "+v"(qse), "+v"(qsw));
+      // W rays: the table ray minus the ray beyond its first blocker (gen_ray<3>)
+      const u64 r0w2 = T.ray[3][msb((r0w & occ) | 1ull)], r1w2 = T.ray[3][msb((r1w & occ) | 1ull)];
+      const u64 qw2 = T.ray[3][msb((qw & occ) | 1ull)];
+      auto up = [](u64 r, u64 o) {  // gen_ray_up on a table ray already read
+        const u64 bl = r & o;
+        return r & (bl ^ (bl - 1));
+      };
+      auto put = [&](int j, bool any, int sv, u32 c) {
+        c = any ? c : 0u;
+        sl[j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
+        n += c;
+      };
+      put(0, an0, n0, pc(tn0 & no));
+      put(1, an1, n1, pc(tn1 & no));
+      put(2, ak, k0, pc(tk & no));
+      put(3, ab0, b0, pc((up(b0ne, occ) | up(b0nw, occ)) & no) + pc((up(b0se, occF) | up(b0sw, occF)) & noF));
+      put(4, ab1, b1, pc((up(b1ne, occ) | up(b1nw, occ)) & no) + pc((up(b1se, occF) | up(b1sw, occF)) & noF));
+      put(5, ar0, r0, pc((up(r0n, occ) | up(r0e, occ) | (r0w ^ r0w2)) & no) + pc(up(r0s, occF) & noF));
+      put(6, ar1, r1, pc((up(r1n, occ) | up(r1e, occ) | (r1w ^ r1w2)) & no) + pc(up(r1s, occF) & noF));
+      put(7, aq, q0,
+          pc((up(qn, occ) | up(qe, occ) | (qw ^ qw2) | up(qne, occ) | up(qnw, occ)) & no) +
+              pc((up(qs, occF) | up(qse, occF) | up(qsw, occF)) & noF));
+    }
+#else
     {
       u64 rem = sw.N;
 #pragma unroll
@@ -856,7 +952,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
         int sv;
         const bool any = take(rem, sv);
         u32 c = 0;
-        if (any) {  // skipped by a wave none of whose games has a j-th such slider
+        if (DC_GEN_NOBR || any) {  // (DC_GEN_NOBR = 0: skipped by a wave none of whose games has a j-th such slider)
 #if DC_GEN_POSRAY
           const int sf = sv ^ 56;  // SW / SE are NW / NE of the flipped board
           c = pc((gen_ray_up<4>(T, sv, occ) | gen_ray_up<6>(T, sv, occ)) & no) +
@@ -866,6 +962,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
           c = pc(t & no);
 #endif
         }
+        c = any ? c : 0u;
         sl[3 + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
@@ -875,7 +972,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
         int sv;
         const bool any = take(rem, sv);
         u32 c = 0;
-        if (any) {
+        if (DC_GEN_NOBR || any) {
 #if DC_GEN_POSRAY
           c = pc((gen_ray_up<0>(T, sv, occ) | gen_ray_up<2>(T, sv, occ) | gen_ray<3>(T, sv, occ)) & no) +
               pc(gen_ray_up<0>(T, sv ^ 56, occF) & noF);  // S: N of the flipped board
@@ -884,6 +981,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
           c = pc(t & no);
 #endif
         }
+        c = any ? c : 0u;
         sl[3 + kGenLine + j] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
@@ -893,7 +991,7 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
         int sv;
         const bool any = take(rem, sv);
         u32 c = 0;
-        if (any) {
+        if (DC_GEN_NOBR || any) {
           const int sf = sv ^ 56;
 #if DC_GEN_POSRAY
           c = pc((gen_ray_up<0>(T, sv, occ) | gen_ray_up<2>(T, sv, occ) | gen_ray<3>(T, sv, occ) |
@@ -906,11 +1004,13 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
           c = pc(t & no);
 #endif
         }
+        c = any ? c : 0u;
         sl[kGenSlots - 1] = any ? (((u32)sv ^ flip) << 8) | c : 64u << 8;
         n += c;
       }
 #endif
     }
+#endif
     if (over) n = 0;
     over = n == 0;
     u64 r = 0;
@@ -944,8 +1044,25 @@ __global__ __launch_bounds__(256, DC_GEN_MINW) void k_gen_games_ref(u64 seed, u6
     // targets of the piece on fv (view), every class masked by its kind
     u64 tv = (((S1 & bit) != 0) ? sh<8>(bit) : 0ull) | (((S2 & bit) != 0) ? sh<16>(bit) : 0ull) |
              (((SL & bit) != 0) ? sh<7>(bit) : 0ull) | (((SR & bit) != 0) ? sh<9>(bit) : 0ull);
+#if DC_GEN_BATCH
+    // every table row of fv read together (the piece's kind selects them after)
+    u64 xn = T.kn[fv], xk = T.kg[fv], x4 = T.ray[4][fv], x6 = T.ray[6][fv], x4f = T.ray[4][fv ^ 56];
+    u64 x6f = T.ray[6][fv ^ 56], x0 = T.ray[0][fv], x2 = T.ray[2][fv], x3 = T.ray[3][fv], x0f = T.ray[0][fv ^ 56];
+    asm volatile("" : "+v"(xn), "+v"(xk), "+v"(x4), "+v"(x6), "+v"(x4f), "+v"(x6f), "+v"(x0), "+v"(x2), "+v"(x3), "+v"(x0f));
+    const u64 x3b = T.ray[3][msb((x3 & occ) | 1ull)];
+    auto upr = [](u64 r, u64 o) {
+      const u64 bl = r & o;
+      return r & (bl ^ (bl - 1));
+    };
+    const u64 md = (sw.D & bit) != 0 ? ~0ull : 0ull, mo = (sw.O & bit) != 0 ? ~0ull : 0ull;
+    u64 tp = ((sw.N & bit) != 0 ? xn : 0ull) | ((sw.K & bit) != 0 ? xk : 0ull);
+    tp |= md & (upr(x4, occ) | upr(x6, occ) | flip_rows(upr(x4f, occF) | upr(x6f, occF)));
+    tp |= mo & (upr(x0, occ) | upr(x2, occ) | (x3 ^ x3b) | flip_rows(upr(x0f, occF)));
+#else
     u64 tp = ((sw.N & bit) != 0 ? T.kn[fv] : 0ull) | ((sw.K & bit) != 0 ? T.kg[fv] : 0ull);
-#if DC_GEN_POSRAY
+#endif
+#if DC_GEN_BATCH
+#elif DC_GEN_POSRAY
     if ((sw.D & bit) != 0)
       tp |= gen_ray_up<4>(T, fv, occ) | gen_ray_up<6>(T, fv, occ) |
             flip_rows(gen_ray_up<4>(T, fv ^ 56, occF) | gen_ray_up<6>(T, fv ^ 56, occF));
