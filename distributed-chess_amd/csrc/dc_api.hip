@@ -187,6 +187,7 @@ struct dc_ctx {
   DBuf<uint16_t> moves;
   DBuf<uint8_t> verdicts, info;
   DBuf<uint8_t> replay_info;  // dc_replay_info / the state hash's first pass: ply-major [n_plies][n_games] move info
+  DBuf<Board> hash_boards;    // the state hash's first pass: every game's final board (round 6)
   DBuf<char> hash_text;    // escaped start history | escaped names of dc_state_hash*
   DBuf<u32> hash_off;      // the names' escaped offsets into hash_text
   DBuf<u32> esc_lens;      // device escaping scratch: per-name escaped lengths,
@@ -256,6 +257,7 @@ struct dc_ctx {
     verdicts.release();
     info.release();
     replay_info.release();
+    hash_boards.release();
     hash_text.release();
     hash_off.release();
     esc_lens.release();
@@ -1130,25 +1132,31 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
   // The pre-pass is an optimisation: when its buffers (up to ~2 GiB near the
   // move bound) cannot be had, or exceed the context's pre-pass budget (a test
   // hook), the hash kernel validates on its own instead of the call failing.
-  const u64 pre_bytes = (u64)n_games * n_plies + 8 * (5 + 5 * (u64)dc::replay_partials(n_games));
+  // (round 6: the pass also leaves every game's final board, 32 B a game,
+  // so the hash kernel makes no move)
+  const u64 pre_bytes = (u64)n_games * n_plies + 8 * (5 + 5 * (u64)dc::replay_partials(n_games)) +
+                        sizeof(Board) * (u64)n_games;
   bool pre = DC_HASH_PRE && n_plies > 0 && (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull &&
              pre_bytes <= c->hash_prepass_max;
   if (pre && (c->replay_info.ensure((size_t)n_games * n_plies) != hipSuccess ||
+              c->hash_boards.ensure(n_games) != hipSuccess ||
               c->stats5.ensure(5 + 5 * (size_t)dc::replay_partials(n_games)) != hipSuccess)) {
     (void)hipGetLastError();
     pre = false;
   }
+  const Board* d_boards = nullptr;
   if (pre) {
     bool host_written = false;
     HIP_TRY(c->timed("state_hash_replay", (u64)n_games * n_plies, [&] {
       return dc::launch_replay_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, nullptr, nullptr, c->stats5.p,
-                                   c->stats5.p + 5, nullptr, &host_written, c->replay_info.p);
+                                   c->stats5.p + 5, nullptr, &host_written, c->replay_info.p, c->hash_boards.p);
     }));
     d_info = c->replay_info.p;
+    d_boards = c->hash_boards.p;
   }
   HIP_TRY(c->timed("state_hash", n_games, [&] {
     return dc::launch_state_hash_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, text, hist_len, hist_tokens,
-                                     text, c->hash_off.p, d_info, d_hashes);
+                                     text, c->hash_off.p, d_info, d_hashes, d_boards);
   }));
   return sync_ctx(c);
 }

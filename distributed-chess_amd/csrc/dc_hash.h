@@ -7,7 +7,10 @@ namespace dc {
 // start history JSON-escaped, names_off[2 n_games + 1] (white_g, black_g pairs).
 hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                                  u32 n_plies, const char* hist, u32 hist_len, u32 hist_tokens, const char* names,
-                                 const u32* names_off, const uint8_t* info, uint8_t* out);
+                                 const u32* names_off, const uint8_t* info, uint8_t* out,
+                                 const Board* final_boards = nullptr);
+// (final_boards, with info: every game's final board from the replay kernel's
+// info pass, so the hash kernel makes no move itself)
 // serde_json escaping of n_str raw UTF-8 strings names[off[i] .. off[i+1]) on
 // the device, in two steps so the host can size the output in between:
 //   len_scan: esc64[i] = base + escaped length of strings 0..i-1 (i <= n_str;

@@ -95,11 +95,27 @@ constexpr JsonTpl make_json_tpl() {
   return t;
 }
 __constant__ JsonTpl g_json_tpl = make_json_tpl();
+constexpr JsonTpl kJsonTpl = make_json_tpl();
+constexpr u32 kCellNullOff = kJsonTpl.off[T_NULL], kCellNullLen = kJsonTpl.len[T_NULL];
+constexpr u32 kCell0Off = kJsonTpl.off[T_CELL0], kCellLen = kJsonTpl.len[T_CELL0];
+constexpr bool cells_even() {
+  for (int k = 1; k < 12; ++k)
+    if (kJsonTpl.len[T_CELL0 + k] != kCellLen || kJsonTpl.off[T_CELL0 + k] != kCell0Off + k * kCellLen) return false;
+  return true;
+}
+static_assert(cells_even(), "the 12 piece-cell templates are consecutive and of one length");
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
 __device__ __forceinline__ u32 kind_index(u32 code) {
   return code == KC_P ? 0 : code == KC_N ? 1 : code == KC_B ? 2 : code == KC_R ? 3 : code == KC_Q ? 4
        : code == KC_K ? 5 : 6;
+}
+
+// a + 2 on packed BCD (15 digits; the move numbers stay below 2^33)
+__device__ __forceinline__ u64 bcd_add2(u64 a) {
+  const u64 t1 = a + 0x0666666666666666ull, t2 = t1 + 2, t3 = t1 ^ 2;
+  const u64 t5 = ~(t2 ^ t3) & 0x1111111111111110ull;  // the digits that carried
+  return t2 - ((t5 >> 2) | (t5 >> 3));
 }
 
 constexpr u32 kHashThreads = 256;
@@ -134,7 +150,8 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
                                                                   u32 hist_tokens, const char* __restrict__ names,
                                                                   const u32* __restrict__ names_off,
                                                                   const uint8_t* __restrict__ info,
-                                                                  uint8_t* __restrict__ out) {
+                                                                  uint8_t* __restrict__ out,
+                                                                  const Board* __restrict__ fboards) {
   // templates and the lanes' move tokens in one LDS pool (a piece in LDS is an
   // offset into it; names and the start history are global pointers)
   constexpr u32 kTplBytes = sizeof(g_json_tpl.s);
@@ -177,8 +194,16 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   // in LDS, names and the start history in global memory, all read through
   // generic (flat) pointers so the byte copy has one code path.  A piece is
   // chosen once (the divergent part) and then copied in runs.
-  Board b = start;
+  // fboards (round 6, with info): the final board comes from the replay
+  // kernel's info pass, so no move is made here (the tokens need only the
+  // info bytes; ref_make per accepted move was 5 % of the kernel's issue)
+  Board b = (fboards && active) ? fboards[g] : start;
   u32 cur = stm0, ply = 0, ntok = hist_tokens;
+  // the move number ntok + 1 as packed BCD, one decimal digit per nibble,
+  // advanced by a BCD add per token (round 6: the divisions by 10 of the
+  // digit loop were 5.8 % of the kernel's issue, tools/bbprof.py)
+  u64 bcd = 0;
+  for (u32 v = hist_tokens + 1, sh = 0; v; v /= 10, sh += 4) bcd |= (u64)(v % 10) << sh;
   u32 stage = active ? S_TURN : S_DONE;
   // the current piece: lpool[loff...] (glb false) or src[...] (glb true)
   const char* src = nullptr;
@@ -241,15 +266,11 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             const bool cap = info ? (code & 8u) != 0 : ((occupied(b) >> t) & 1) != 0;
             u32 n = 0;
             if (ntok) mytok[n++] = ' ';
-            // N's decimal digits written last-first straight into the token
-            // (round 4 built them in a dynamically indexed register array:
-            // 29 % of the kernel's issue cycles in tools/bbprof.py's count)
-            u32 v = ntok + 1, nd = 1;
-            for (u32 q = v; q >= 10; q /= 10) ++nd;
-            for (u32 i = nd; i-- > 0;) {
-              mytok[n + i] = (char)('0' + v % 10);
-              v /= 10;
-            }
+            // N's decimal digits straight into the token from the BCD (round 4
+            // built them in a dynamically indexed register array: 29 % of the
+            // kernel's issue cycles in tools/bbprof.py's count)
+            const u32 nd = max(1u, (67u - (u32)__clzll((long long)bcd)) >> 2);
+            for (u32 i = 0; i < nd; ++i) mytok[n + i] = (char)('0' + (u32)((bcd >> (4 * (nd - 1 - i))) & 15));
             n += nd;
             mytok[n++] = '.';
             mytok[n++] = ' ';
@@ -260,9 +281,10 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             }
             mytok[n++] = (char)('a' + (t & 7));
             mytok[n++] = (char)('1' + (t >> 3));
-            ref_make(b, f, t);
+            if (!fboards) ref_make(b, f, t);  // (kernel-uniform)
             cur ^= 1;
             ntok += 2;
+            bcd = bcd_add2(bcd);
             glb = false;
             loff = tok_off;
             rem = n;
@@ -299,8 +321,12 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           stage = S_CELL;
           const u32 nib = nibble(b, (int)(8 * row + col));
           const u32 ki = kind_index(nib >> 1);
-          const int ti = (nib >> 1) == 0 ? (int)T_NULL : (int)T_CELL0 + 6 * (int)(nib & 1) + (ki < 6 ? (int)ki : 0);
-          tpl_piece(ti, col == 7 ? 1u : 0u);
+          // the cell templates' offsets and lengths as constants (round 6:
+          // the per-lane index into g_json_tpl made two global loads a cell)
+          const u32 k = 6 * (nib & 1) + (ki < 6 ? ki : 0);
+          glb = false;
+          loff = (nib >> 1) == 0 ? kCellNullOff : kCell0Off + kCellLen * k;
+          rem = ((nib >> 1) == 0 ? kCellNullLen : kCellLen) - (col == 7 ? 1u : 0u);
           break;
         }
         default:  // S_END
@@ -453,10 +479,11 @@ hipError_t launch_escape_write(hipStream_t st, const char* names, const u32* off
 
 hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                                  u32 n_plies, const char* hist, u32 hist_len, u32 hist_tokens, const char* names,
-                                 const u32* names_off, const uint8_t* info, uint8_t* out) {
+                                 const u32* names_off, const uint8_t* info, uint8_t* out, const Board* final_boards) {
   if (n_games == 0) return hipSuccess;
   hipLaunchKernelGGL(k_state_hash_ref, dim3(blocks_for(n_games, kHashThreads)), dim3(kHashThreads), 0, st, start, stm0,
-                     moves, n_games, n_plies, hist, hist_len, hist_tokens, names, names_off, info, out);
+                     moves, n_games, n_plies, hist, hist_len, hist_tokens, names, names_off, info, out,
+                     info ? final_boards : nullptr);
   return hipGetLastError();
 }
 

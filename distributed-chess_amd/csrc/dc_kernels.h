@@ -116,7 +116,9 @@ hipError_t launch_apply_ref(hipStream_t st, DevPos* pos, const uint16_t* moves, 
 u32 replay_partials(u32 n_games);
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                              u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial, u64* stats_host,
-                             bool* host_written, uint8_t* info = nullptr);
+                             bool* host_written, uint8_t* info = nullptr, Board* boards = nullptr);
+// (info != nullptr: the per-ply info form; boards != nullptr then also
+// receives every game's final board, the state hash's board JSON)
 hipError_t launch_gen_games_ref(hipStream_t st, u64 seed, u64 first_game, u32 n_games, u32 n_plies, u32 noise,
                                 uint16_t* out);
 }  // namespace dc

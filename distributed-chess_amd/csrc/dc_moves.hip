@@ -435,7 +435,8 @@ template <int LOOK, int PF, bool DW, bool INFO = false>
 __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ0, u32 stm0, const uint16_t* __restrict__ moves,
                                                            u32 n_games, u32 n_plies, u64* __restrict__ bitmap,
                                                            u64* __restrict__ digests, u64* __restrict__ partial,
-                                                           uint8_t* __restrict__ info = nullptr) {
+                                                           uint8_t* __restrict__ info = nullptr,
+                                                           Board* __restrict__ boards = nullptr) {
   __shared__ __attribute__((aligned(16))) unsigned char r4_smem[kR3TabBytes + kR3MbBytes];
   u64* btw = reinterpret_cast<u64*>(r4_smem);
   u32* mb = reinterpret_cast<u32*>(r4_smem + kR3TabBytes);
@@ -592,6 +593,7 @@ __global__ __launch_bounds__(kR3Threads) void k_replay_ref4(Mailbox mb0, u64 occ
       if (DC_R4_LAZY) b = Board{b.b0 & occ, b.b1 & occ, b.b2 & occ, b.b3 & occ};  // stale nibbles of vacated squares
       const u64 dg = board_digest(b, stm);
       if (digests) digests[g] = dg;
+      if (INFO && boards) boards[g] = b;  // the state hash's final boards (round 6)
       dsum += dg;
       dxor ^= dg;
     }
@@ -1432,7 +1434,7 @@ static Mailbox host_mailbox(const Board& b) {
 
 hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                              u32 n_plies, u64* bitmap, u64* digests, u64* stats, u64* partial, u64* stats_host,
-                             bool* host_written, uint8_t* info) {
+                             bool* host_written, uint8_t* info, Board* boards) {
   *host_written = false;
   if (n_games == 0) return hipSuccess;
   if (info && n_plies > 0) {  // the resync path: k_replay_ref4<.., INFO> (one buffer descriptor: < 4 GiB of moves)
@@ -1441,7 +1443,7 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
     const bool dw = (n_games & 1) == 0;
     auto ki = dw ? k_replay_ref4<0, 4, true, true> : k_replay_ref4<0, 4, false, true>;
     hipLaunchKernelGGL(ki, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start), start.b1 | start.b2 | start.b3,
-                       stm0, moves, n_games, n_plies, bitmap, digests, partial, info);
+                       stm0, moves, n_games, n_plies, bitmap, digests, partial, info, boards);
     hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(256), 0, st, partial, nb, stats, stats_host);
     *host_written = stats_host != nullptr;
     return hipGetLastError();
@@ -1469,7 +1471,7 @@ hipError_t launch_replay_ref(hipStream_t st, const Board& start, u32 stm0, const
     const bool fits = (u64)n_games * n_plies * 2 <= 0xFFFFFFFFull;
     if (fits && !force3)
       hipLaunchKernelGGL(k4, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start), start.b1 | start.b2 | start.b3,
-                         stm0, moves, n_games, n_plies, bitmap, digests, partial, nullptr);
+                         stm0, moves, n_games, n_plies, bitmap, digests, partial, nullptr, nullptr);
     else
       hipLaunchKernelGGL(k_replay_ref3, dim3(nb), dim3(kR3Threads), 0, st, host_mailbox(start),
                          start.b1 | start.b2 | start.b3, stm0, moves, n_games, n_plies, bitmap, digests, partial);
