@@ -201,6 +201,9 @@ struct dc_ctx {
   // the state hash's replay pre-pass is skipped past this many bytes of its
   // buffers (unlimited; dc_test_hash_prepass_max lowers it to test the fallback)
   u64 hash_prepass_max = ~0ull;
+  // the hash kernel keeps move numbers as 32-bit BCD below this bound (at most
+  // 10^7; dc_test_hash_bcd_max lowers it to test the division fallback)
+  u32 hash_bcd_max = 10000000u;
   DBuf<u32> move_words;  // k_count3c: the final stage's parents as move words below their grandparents
   DBuf<u64> move_words64;  // ... as 64-bit words (REF perft(8): more than 2^20 grandparents)
   DBuf<dc::Range> slice_rng;  // the sliced final stage (REF perft(9)): one slice's node and word Ranges
@@ -711,6 +714,14 @@ extern "C" __attribute__((visibility("default"))) int dc_test_hash_prepass_max(d
   return DC_SUCCESS;
 }
 
+// Test hook (not in the header): the state hash's BCD move-number bound
+// (clamped to 10^7), so a test can force the kernel's division path.
+extern "C" __attribute__((visibility("default"))) int dc_test_hash_bcd_max(dc_ctx* c, uint32_t bound) {
+  if (!c) return DC_EINVAL;
+  c->hash_bcd_max = bound < 10000000u ? bound : 10000000u;
+  return DC_SUCCESS;
+}
+
 // One request through the mailbox.  pos_out (apply) may alias pos.
 // The whole call runs under g_live_mu (then c->live_mu), and whether a hold is
 // active is decided under that lock: a LiveHold counts itself before it takes
@@ -1077,7 +1088,7 @@ u32 count_ws_tokens(const char* s, size_t n) {
 // k_escape_len / k_escape_write); hash_off = the names' escaped offsets.  One
 // small readback sizes hash_text from the exact escaped total.
 int stage_hash_text(dc_ctx* c, const char* history, const char* d_names, const uint32_t* d_names_off, uint32_t n_games,
-                    u32* hist_len, u32* hist_tokens) {
+                    u32* hist_len, u32* hist_tokens, const char** names_out, const u32** off_out) {
   const size_t hn = history ? std::strlen(history) : 0;
   c->hist_text.clear();
   json_escape(history ? history : "", hn, c->hist_text);
@@ -1086,8 +1097,23 @@ int stage_hash_text(dc_ctx* c, const char* history, const char* d_names, const u
   *hist_tokens = count_ws_tokens(history ? history : "", hn);
   const u64 n_str = 2ull * n_games;
   if (n_str + 1 > 0x7FFFFFFFull) return DC_EUNSUPPORTED;  // hipcub's item count is an int
-  const size_t tb = dc::escape_scan_tmp_bytes((u32)n_str);
+  // Fast path (round 6): names with no byte to escape and ordered offsets are
+  // their own serde_json escapes; the hash kernel then reads them in place and
+  // the escaping kernels, scan and copy (~80 us per 1M games) are skipped.
   HIP_TRY(c->esc_lens.ensure(n_str + 1));
+  HIP_TRY(dc::launch_names_plain(c->stream, d_names, d_names_off, (u32)n_str, c->esc_lens.p));
+  u32 escapes = 1;
+  HIP_TRY(hipMemcpyAsync(&escapes, c->esc_lens.p, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (!escapes) {
+    HIP_TRY(c->hash_text.ensure(std::max<size_t>(*hist_len, 1)));
+    if (*hist_len)
+      HIP_TRY(hipMemcpyAsync(c->hash_text.p, c->hist_text.data(), *hist_len, hipMemcpyHostToDevice, c->stream));
+    *names_out = d_names;
+    *off_out = d_names_off;
+    return DC_SUCCESS;
+  }
+  const size_t tb = dc::escape_scan_tmp_bytes((u32)n_str);
   HIP_TRY(c->esc64.ensure(n_str + 1));
   HIP_TRY(c->scan_tmp.ensure(std::max<size_t>(tb, 1)));
   HIP_TRY(c->hash_off.ensure(n_str + 1));
@@ -1102,6 +1128,8 @@ int stage_hash_text(dc_ctx* c, const char* history, const char* d_names, const u
     HIP_TRY(hipMemcpyAsync(c->hash_text.p, c->hist_text.data(), *hist_len, hipMemcpyHostToDevice, c->stream));
   HIP_TRY(dc::launch_escape_write(c->stream, d_names, d_names_off, (u32)n_str, c->esc64.p, c->hash_off.p,
                                   c->hash_text.p));
+  *names_out = c->hash_text.p;
+  *off_out = c->hash_off.p;
   return DC_SUCCESS;
 }
 
@@ -1116,11 +1144,7 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
   // pieces of unknown kind keep a proto kind string this engine does not know
   if (s0.bb[3] & ~(s0.bb[1] | s0.bb[2])) return DC_EUNSUPPORTED;
   if (n_games == 0) return DC_SUCCESS;
-  u32 hist_len = 0, hist_tokens = 0;
-  int e = stage_hash_text(c, history, d_names, d_names_off, n_games, &hist_len, &hist_tokens);
-  if (e != DC_SUCCESS) return e;
   const Board b{s0.bb[0], s0.bb[1], s0.bb[2], s0.bb[3]};
-  const char* text = c->hash_text.p;
   // The replay kernel first (round 5): its per-ply info byte (dc_replay_info's
   // form) gives the hash kernel each ply's verdict, mover kind and capture, so
   // the hash kernel validates nothing.  Batches past the replay kernel's one
@@ -1154,9 +1178,17 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
     d_info = c->replay_info.p;
     d_boards = c->hash_boards.p;
   }
+  // the names staged after the pass is enqueued: the staging's one readback
+  // then waits on the pass's GPU time instead of idling the GPU (round 6)
+  u32 hist_len = 0, hist_tokens = 0;
+  const char* names = nullptr;
+  const u32* names_off = nullptr;
+  int e = stage_hash_text(c, history, d_names, d_names_off, n_games, &hist_len, &hist_tokens, &names, &names_off);
+  if (e != DC_SUCCESS) return e;
+  const char* text = c->hash_text.p;
   HIP_TRY(c->timed("state_hash", n_games, [&] {
     return dc::launch_state_hash_ref(c->stream, b, s0.stm, d_moves, n_games, n_plies, text, hist_len, hist_tokens,
-                                     text, c->hash_off.p, d_info, d_hashes, d_boards);
+                                     names, names_off, d_info, d_hashes, d_boards, c->hash_bcd_max);
   }));
   return sync_ctx(c);
 }

@@ -111,10 +111,10 @@ __device__ __forceinline__ u32 kind_index(u32 code) {
        : code == KC_K ? 5 : 6;
 }
 
-// a + 2 on packed BCD (15 digits; the move numbers stay below 2^33)
-__device__ __forceinline__ u64 bcd_add2(u64 a) {
-  const u64 t1 = a + 0x0666666666666666ull, t2 = t1 + 2, t3 = t1 ^ 2;
-  const u64 t5 = ~(t2 ^ t3) & 0x1111111111111110ull;  // the digits that carried
+// a + 2 on 32-bit packed BCD (7 digits: callers keep the numbers below 10^7)
+__device__ __forceinline__ u32 bcd_add2(u32 a) {
+  const u32 t1 = a + 0x06666666u, t2 = t1 + 2, t3 = t1 ^ 2;
+  const u32 t5 = ~(t2 ^ t3) & 0x11111110u;  // the digits that carried
   return t2 - ((t5 >> 2) | (t5 >> 3));
 }
 
@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
                                                                   const u32* __restrict__ names_off,
                                                                   const uint8_t* __restrict__ info,
                                                                   uint8_t* __restrict__ out,
-                                                                  const Board* __restrict__ fboards) {
+                                                                  const Board* __restrict__ fboards, u32 bcd_max) {
   // templates and the lanes' move tokens in one LDS pool (a piece in LDS is an
   // offset into it; names and the start history are global pointers)
   constexpr u32 kTplBytes = sizeof(g_json_tpl.s);
@@ -202,8 +202,11 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   // the move number ntok + 1 as packed BCD, one decimal digit per nibble,
   // advanced by a BCD add per token (round 6: the divisions by 10 of the
   // digit loop were 5.8 % of the kernel's issue, tools/bbprof.py)
-  u64 bcd = 0;
-  for (u32 v = hist_tokens + 1, sh = 0; v; v /= 10, sh += 4) bcd |= (u64)(v % 10) << sh;
+  // (32-bit: every number of the batch below bcd_max <= 10^7, else the divisions)
+  const bool bcd_ok = (u64)hist_tokens + 2ull * n_plies + 1 < (u64)min(bcd_max, 10000000u);  // kernel-uniform
+  u32 bcd = 0;
+  if (bcd_ok)
+    for (u32 v = hist_tokens + 1, sh = 0; v; v /= 10, sh += 4) bcd |= (v % 10) << sh;
   u32 stage = active ? S_TURN : S_DONE;
   // the current piece: lpool[loff...] (glb false) or src[...] (glb true)
   const char* src = nullptr;
@@ -269,9 +272,19 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             // N's decimal digits straight into the token from the BCD (round 4
             // built them in a dynamically indexed register array: 29 % of the
             // kernel's issue cycles in tools/bbprof.py's count)
-            const u32 nd = max(1u, (67u - (u32)__clzll((long long)bcd)) >> 2);
-            for (u32 i = 0; i < nd; ++i) mytok[n + i] = (char)('0' + (u32)((bcd >> (4 * (nd - 1 - i))) & 15));
-            n += nd;
+            if (bcd_ok) {
+              const u32 nd = max(1u, (35u - (u32)__clz((int)bcd)) >> 2);
+              for (u32 i = 0; i < nd; ++i) mytok[n + i] = (char)('0' + __builtin_amdgcn_ubfe(bcd, 4 * (nd - 1 - i), 4));
+              n += nd;
+            } else {  // digits written last-first
+              u32 v = ntok + 1, nd = 1;
+              for (u32 q = v; q >= 10; q /= 10) ++nd;
+              for (u32 i = nd; i-- > 0;) {
+                mytok[n + i] = (char)('0' + v % 10);
+                v /= 10;
+              }
+              n += nd;
+            }
             mytok[n++] = '.';
             mytok[n++] = ' ';
             if (ki != 0) mytok[n++] = "PNBRQK"[ki];
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             if (!fboards) ref_make(b, f, t);  // (kernel-uniform)
             cur ^= 1;
             ntok += 2;
-            bcd = bcd_add2(bcd);
+            if (bcd_ok) bcd = bcd_add2(bcd);
             glb = false;
             loff = tok_off;
             rem = n;
@@ -457,6 +470,30 @@ __global__ __launch_bounds__(256) void k_escape_write(const char* __restrict__ n
   }
 }
 
+// The fast path's check (round 6): flag[0] = 1 if any byte of names[0 ..
+// off[n_str]) needs a JSON escape or an offset decreases; else the names are
+// their own serde_json escapes and the hash kernel reads them in place (no
+// per-name scan and copy).  Byte-parallel and coalesced.
+__global__ __launch_bounds__(256) void k_names_plain(const char* __restrict__ names, const u32* __restrict__ off,
+                                                    u32 n_str, u32* __restrict__ flag) {
+  const u64 total = off[n_str];
+  const u64 stride = (u64)gridDim.x * blockDim.x;
+  bool bad = false;
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += stride) {
+    const u32 ch = (unsigned char)names[i];
+    bad |= ch < 0x20 || ch == '"' || ch == '\\';
+  }
+  for (u64 i = (u64)blockIdx.x * blockDim.x + threadIdx.x; i < n_str; i += stride) bad |= off[i] > off[i + 1];
+  if (__ballot(bad) != 0 && lane_id() == 0) atomicOr(flag, 1u);
+}
+
+hipError_t launch_names_plain(hipStream_t st, const char* names, const u32* off, u32 n_str, u32* flag) {
+  hipError_t e = hipMemsetAsync(flag, 0, sizeof(u32), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_names_plain, dim3(2048), dim3(256), 0, st, names, off, n_str, flag);
+  return hipGetLastError();
+}
+
 size_t escape_scan_tmp_bytes(u32 n_str) {
   size_t bytes = 0;
   (void)hipcub::DeviceScan::ExclusiveScan(nullptr, bytes, (const u32*)nullptr, (u64*)nullptr, hipcub::Sum(), (u64)0,
@@ -479,11 +516,12 @@ hipError_t launch_escape_write(hipStream_t st, const char* names, const u32* off
 
 hipError_t launch_state_hash_ref(hipStream_t st, const Board& start, u32 stm0, const uint16_t* moves, u32 n_games,
                                  u32 n_plies, const char* hist, u32 hist_len, u32 hist_tokens, const char* names,
-                                 const u32* names_off, const uint8_t* info, uint8_t* out, const Board* final_boards) {
+                                 const u32* names_off, const uint8_t* info, uint8_t* out, const Board* final_boards,
+                                 u32 bcd_max) {
   if (n_games == 0) return hipSuccess;
   hipLaunchKernelGGL(k_state_hash_ref, dim3(blocks_for(n_games, kHashThreads)), dim3(kHashThreads), 0, st, start, stm0,
                      moves, n_games, n_plies, hist, hist_len, hist_tokens, names, names_off, info, out,
-                     info ? final_boards : nullptr);
+                     info ? final_boards : nullptr, bcd_max);
   return hipGetLastError();
 }
 

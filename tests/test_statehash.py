@@ -157,6 +157,30 @@ def test_state_hash_without_replay_prepass(engine):
 
 
 @pytest.mark.gpu
+def test_state_hash_move_numbers_by_division(engine):
+    """The hash kernel keeps the history's move numbers as 32-bit BCD when
+    every number of the batch stays below 10^7, else it divides by 10; the
+    test hook dc_test_hash_bcd_max lowers that bound so the division path runs
+    (a start history of several tokens, numbers into three digits), with the
+    same hashes as the BCD path and the oracle."""
+    import ctypes as C
+    import oracle_lib as O
+    L = dchess.lib()
+    L.dc_test_hash_bcd_max.argtypes = [C.c_void_p, C.c_uint32]
+    mv = _games(14, 40, 61, O.Pos())
+    names = [(NAMES[g % len(NAMES)], "b" + str(g)) for g in range(40)]
+    history = "1. e4 e5 2. Nf3 " + " ".join(str(k) for k in range(40))
+    bcd = engine.state_hash(mv, names, history=history)
+    try:
+        assert L.dc_test_hash_bcd_max(engine.ctx, 1) == 0
+        div = engine.state_hash(mv, names, history=history)
+    finally:
+        L.dc_test_hash_bcd_max(engine.ctx, 10**7)
+    assert (bcd == div).all()
+    assert (div == _oracle_hashes(O.Pos(), history, names, mv)).all()
+
+
+@pytest.mark.gpu
 def test_state_hash_matches_gamestate_mirror(engine):
     """One game through the Python GameState mirror (dc_apply_batch per move,
     host JSON + dc_keccak256) and through the batched kernel."""
@@ -211,6 +235,33 @@ def test_state_hash_device_resident_names(engine):
     assert (engine.state_hash(mv, names, history=history) == want).all()
     for b in (d_names, d_off, d_moves, d_h):
         b.free()
+
+
+@pytest.mark.gpu
+def test_state_hash_plain_names_read_in_place(engine):
+    """Names with no byte serde_json escapes (ASCII letters, digits, 0x7f,
+    multi-byte UTF-8, empty names) take the fast path: k_names_plain finds
+    nothing to escape and the hash kernel reads the raw names and offsets in
+    place.  Checked against the oracle, with a start history that is escaped
+    (its own path), and against a batch where one name needs an escape."""
+    import oracle_lib as O
+    start = O.Pos()
+    n_games, n_plies = 70, 19
+    mv = _games(31, n_games, n_plies, start)
+    pool = ["Alice", "Bob", "Ümlaut ♞ 名前", "", "a" * 300, "x\x7fy", "white123456"]
+    names = [(pool[g % len(pool)], pool[(g * 3 + 2) % len(pool)] + str(g)) for g in range(n_games)]
+    history = "1. e4 e5\t"
+    for nm in (names, names[:-1] + [("tab\there", "q\"")]):
+        blob, off = dchess.pack_names(nm)
+        d_names, d_off = engine.names_device(blob, off)
+        d_moves = engine.alloc(mv.nbytes)
+        d_moves.upload(mv)
+        d_h = engine.alloc(32 * n_games)
+        engine.state_hash_device(d_moves, n_games, n_plies, d_names, d_off, d_h, history=history)
+        got = d_h.download(np.uint8, 32 * n_games).reshape(n_games, 32)
+        assert (got == _oracle_hashes(start, history, nm, mv)).all()
+        for b in (d_names, d_off, d_moves, d_h):
+            b.free()
 
 
 @pytest.mark.gpu
