@@ -49,7 +49,7 @@ if has pmc; then
   python tools/pmc_summary.py $O --json $O/pmc_latest.json --source "rocprofv3 --pmc (4 passes), bench.py $P" \
     --units "final_d7=k_count3c<0&unsigned int=3282734510" --units "final_d8=k_count3c<1&unsigned long=$D8" \
     --units "dfs_d9=k_perft_dfs<=$D9" \
-    --units "replay=k_replay_ref4=799999953" --units "gen_games=k_gen_games_ref=799999953" \
+    --units "replay=k_replay_ref4&true, false>=799999953" --units "gen_games=k_gen_games_ref=799999953" \
     --units "state_hash=k_state_hash_ref=1000000" --units "verify_tx=k_verify_tx=262144" > $O/pmc_summary.txt
 fi
 if has fidepmc; then
