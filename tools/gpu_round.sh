@@ -86,7 +86,7 @@ if has txpmc; then
   tpass "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU" t1 && \
   tpass "FETCH_SIZE" t2 && tpass "WRITE_SIZE" t3 && tpass "SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" t4 && tpass "SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 GRBM_GUI_ACTIVE" t5 || { tail $O/pmc.err; exit 7; }
   mkdir -p $O/tx && mv $O/pmc_t[1-5] $O/tx/
-  python tools/pmc_summary.py $O/tx --json $O/pmc_tx.json --tx-units 262144 --source "rocprofv3 --pmc, bench.py $P" > $O/pmc_tx.txt
+  python tools/pmc_summary.py $O/tx --json $O/pmc_tx.json --units "verify_tx=k_verify_tx=262144" --source "rocprofv3 --pmc, bench.py $P" > $O/pmc_tx.txt
   python - <<'PY'
 import json, os
 p = "gpurun_out/pmc_latest.json"
