@@ -1492,6 +1492,9 @@ extern "C" __attribute__((visibility("default"))) int dc_diag_child_set(void* de
 #ifndef DC_C2B_EVEN
 #define DC_C2B_EVEN 0
 #endif
+#ifndef DC_C2B_GUIDED
+#define DC_C2B_GUIDED 0
+#endif
 template <class R, int STM>
 __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board* __restrict__ nodes, const uint16_t* __restrict__ meta,
                                                     const uint16_t* __restrict__ tags, const Range* __restrict__ rng,
@@ -1523,10 +1526,29 @@ __global__ __launch_bounds__(256, R::kFinalMinBlocks) void k_count2b(const Board
 #else
   const u64 cs = min<u64>(kChunk, share);
 #endif
+#if DC_C2B_GUIDED
+  // DC_C2B_GUIDED (round 6): a level of more than one round of chunks ends in
+  // 64-parent chunks (its last 2 x grid x 64 parents).  A chunk's parent phase
+  // runs one thread per parent, and a wave none of whose threads holds a
+  // parent skips it, so a 64-parent chunk costs one wave's parent phase, not
+  // four; the small chunks let the blocks that finish early take the tail.
+  // Measured slower (profiles/r06/ab_c2b_guided.txt, same box, alternating):
+  // the suite step 0.329-0.333 -> 0.345-0.347 ms.  Off (A/B knob).
+  constexpr u64 kTail = 64;
+  const u64 nlev = hi - lo;
+  const u64 tail = share > kChunk ? min<u64>(nlev, 2ull * gridDim.x * kTail) : 0ull;
+  const u64 nbig = (nlev - tail) / cs, tstart = nbig * cs;
+  const u64 nch = nbig + (nlev - tstart + kTail - 1) / kTail * (tail ? 1 : 0) + (tail ? 0 : (nlev - tstart + cs - 1) / cs);
+  for (u64 c = blockIdx.x; c < nch;) {  // block-uniform
+    const bool big = c < nbig || !tail;
+    const u64 s = lo + (big ? c * cs : tstart + (c - nbig) * kTail);
+    const u64 bhi = min(hi, s + (big ? cs : kTail));
+#else
   const u64 nch = (hi - lo + cs - 1) / cs;
   for (u64 c = blockIdx.x; c < nch;) {  // block-uniform
     const u64 s = lo + c * cs;
     const u64 bhi = min(hi, s + cs);
+#endif
 #else
   (void)next_chunk;
   const u64 per = (hi - lo + gridDim.x - 1) / gridDim.x;  // (DC_C2B_DYN=0, and the diagnostic builds)
@@ -2296,6 +2318,9 @@ constexpr u32 kGroup = 256;
 #ifndef DC_C3C_EVEN
 #define DC_C3C_EVEN 0
 #endif
+#ifndef DC_C3C_TAIL
+#define DC_C3C_TAIL 0
+#endif
 #ifndef DC_C3C_LOG
 #define DC_C3C_LOG 0
 #endif
@@ -2352,16 +2377,35 @@ __global__ __launch_bounds__(256, MINW) void k_count3c(const Board* __restrict__
 #else
   constexpr u32 gsz = kGroup;
 #endif
+#if DC_C3C_TAIL
+  // DC_C3C_TAIL (round 6 A/B): a level of more than one round of groups ends
+  // in 64-word groups (its last 2 x grid x 64 words).  A wave none of whose
+  // lanes holds a word skips the parent split, so a 64-word group pays one
+  // wave's split, not four (DC_C3C_EVEN's partial waves paid them all).
+  // Measured slower (profiles/r06/ab_c3tail.jsonl): shard 0 of 8 0.084 ->
+  // 0.099 ms, perft(7) 0.375 -> 0.390 ms on one context; each small group
+  // still pays the block's scans, barriers and pooled queue drains.
+  constexpr u32 kTail = 64;
+  const u32 tail = (total + gridDim.x - 1) / gridDim.x > kGroup ? min(total, 2u * gridDim.x * kTail) : 0u;
+  const u32 nbig = (total - tail) / gsz, tstart = nbig * gsz;
+#endif
   u32 grp = blockIdx.x;
   for (;;) {
     // (fetching the next group's index one group ahead, to take its round
     // trip off the load chain, made the kernel 0.495 -> 0.519 ms at perft(7):
     // a block then holds a group it cannot start, which lengthens the tail)
+#if DC_C3C_TAIL
+    const bool big = grp < nbig || !tail;
+    const u64 s = big ? (u64)grp * gsz : (u64)tstart + (u64)(grp - nbig) * kTail;
+    const u32 gn = big ? gsz : kTail;
+#else
     const u64 s = (u64)grp * gsz;
+    const u32 gn = gsz;
+#endif
     if (s >= total) break;  // block-uniform
     const u32 ot = otid(wave);
     const u64 i = s + ot;
-    const bool valid = ot < gsz && i < total;
+    const bool valid = ot < gn && i < total;
     Board ch{0, 0, 0, 0};
     u32 tag = 0;
     if (valid) {
