@@ -126,7 +126,13 @@ __device__ __forceinline__ void keccak_f1600_dev(uint64_t* a64) {
   K64 a[25];
 #pragma unroll
   for (int i = 0; i < 25; ++i) a[i] = K64{(uint32_t)a64[i], (uint32_t)(a64[i] >> 32)};
-#pragma unroll 1
+// DC_KECCAK_UNROLL (round 6 A/B): rounds per loop trip.  2 and 4 fit the same
+// 3 waves/SIMD (142-144 VGPRs) and measured slower: hash kernel 3.90-3.93 ->
+// 3.99-4.00 ms (2) and 3.93-4.00 ms (4) (profiles/r06/ab_keccak_unroll.txt).
+#ifndef DC_KECCAK_UNROLL
+#define DC_KECCAK_UNROLL 1
+#endif
+#pragma unroll DC_KECCAK_UNROLL
   for (int r = 0; r < 24; ++r) {
     const K64 c0 = kx3(kx3(a[0], a[5], a[10]), a[15], a[20]);
     const K64 c1 = kx3(kx3(a[1], a[6], a[11]), a[16], a[21]);
