@@ -790,6 +790,9 @@ def concurrent_perfts(d, args, items, depth, steps, rules):
     return leaves, dt
 
 
+SUITE_STREAMS = 4
+
+
 def batch_perfts(eng, d, args, items, depth, steps, rules):
     """The positions of a suite as ONE tree (dc_perft_batch_repeat_device: same side
     to move, root moves sharing the divide tags), so every level and the final
@@ -804,7 +807,11 @@ def batch_perfts(eng, d, args, items, depth, steps, rules):
     if [int(x) for x in tot] != want:
         raise SystemExit(f"parity failure: batch FIDE perft({depth}) = {list(tot)}, expected {want}")
     b = eng.alloc(max(REPEAT_BATCH, steps) * W * 8)
-    engs = perft_contexts(eng, d, max(1, min(args.perft_streams or 2, steps)))  # (front end ~80 us of ~0.46 ms)
+    # the steps over SUITE_STREAMS contexts: one batch's final stage ends in a
+    # tail of unevenly costly chunks (938 over 768 blocks) that the other
+    # contexts' runs fill (profiles/r06/suite_streams.txt: 0.330-0.333 ms per
+    # step on 2, 0.301-0.312 on 3, 0.297-0.300 on 4 -- GPU_MAX_HW_QUEUES)
+    engs = perft_contexts(eng, d, max(1, min(args.perft_streams or SUITE_STREAMS, steps)))
 
     def run(e, k, ptr):
         e.perft_batch_repeat_device(pos, depth, args.split, k, ptr, rules=rules)
@@ -889,11 +896,15 @@ def fide_leg(eng, d, args, name, depth, keys, pmc_key):
     if batched:
         out["batch"] = ({"tree": "the positions as one tree (dc_perft_batch_repeat_device: root moves of all "
                                  "positions share the divide tags, every level and the final stage one grid); "
-                                 "final_kernel_ms is that one final stage",
+                                 f"final_kernel_ms is that one final stage; the timed steps are split over "
+                                 f"{args.perft_streams or SUITE_STREAMS} contexts (streams), each step a whole "
+                                 f"batch with its own result record",
                          "streams": "one context (stream) per position, every position's repeat runs enqueued "
                                     "before any wait"}[how] +
                         "; positions[].ms_per_step and sequential_ms_per_step time the positions one after another")
         out["sequential_ms_per_step"] = seq_ms
+        if how == "tree":
+            out["streams_per_gpu"] = args.perft_streams or SUITE_STREAMS
     rec = _pmc(pmc_key) if d.world == 1 else None
     if rec and kl and kms > 0:
         out["roofline"] = valu_roof("k_count2b", kunits / (kms / 1e3), "leaf", W_COUNT2, rec,
