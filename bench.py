@@ -790,7 +790,7 @@ def concurrent_perfts(d, args, items, depth, steps, rules):
     return leaves, dt
 
 
-SUITE_STREAMS = 4
+SUITE_STREAMS = 2
 
 
 def batch_perfts(eng, d, args, items, depth, steps, rules):
@@ -807,10 +807,10 @@ def batch_perfts(eng, d, args, items, depth, steps, rules):
     if [int(x) for x in tot] != want:
         raise SystemExit(f"parity failure: batch FIDE perft({depth}) = {list(tot)}, expected {want}")
     b = eng.alloc(max(REPEAT_BATCH, steps) * W * 8)
-    # the steps over SUITE_STREAMS contexts: one batch's final stage ends in a
-    # tail of unevenly costly chunks (938 over 768 blocks) that the other
-    # contexts' runs fill (profiles/r06/suite_streams.txt: 0.330-0.333 ms per
-    # step on 2, 0.301-0.312 on 3, 0.297-0.300 on 4 -- GPU_MAX_HW_QUEUES)
+    # the steps over SUITE_STREAMS contexts.  (Round 6: four measured 0.297-0.312
+    # ms per step against 0.330 on two in a process that ran only this leg, but
+    # 0.332 against 0.331 after the perft legs had run on the same contexts,
+    # as the default bench does: profiles/r06/suite_streams.txt; so two.)
     engs = perft_contexts(eng, d, max(1, min(args.perft_streams or SUITE_STREAMS, steps)))
 
     def run(e, k, ptr):
