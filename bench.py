@@ -810,7 +810,8 @@ def batch_perfts(eng, d, args, items, depth, steps, rules):
     # the steps over SUITE_STREAMS contexts.  (Round 6: four measured 0.297-0.312
     # ms per step against 0.330 on two in a process that ran only this leg, but
     # 0.332 against 0.331 after the perft legs had run on the same contexts,
-    # as the default bench does: profiles/r06/suite_streams.txt; so two.)
+    # as the default bench does, and 0.326-0.329 on four fresh contexts:
+    # profiles/r06/suite_streams.txt; so two.)
     engs = perft_contexts(eng, d, max(1, min(args.perft_streams or SUITE_STREAMS, steps)))
 
     def run(e, k, ptr):
