@@ -233,7 +233,8 @@ def perft_streams(args, depth, world=1):
     not fill the GPU; with the steps split over two or three contexts --
     streams -- one run's front end executes while another's final stage holds
     the CUs (tools/overlap_perft.py, profiles/r06/overlap_ctx.jsonl, overlap_q:
-    perft(7) 0.376 -> 0.351 ms per step with 2, 0.353 with 3; perft(6) 0.048 ->
+    perft(7) 0.376 -> 0.351 ms per step with 2, 0.353 with 3, 0.361-0.365 with 4
+    (profiles/r06/perft7_streams.txt); perft(6) 0.048 ->
     0.036 with 2 or 3).  A rank of N >= 4 holds a shard whose final stage is
     about as long as its front end, so perft(7) takes 3 there (shard 0 of 8:
     0.085 ms on one context, 0.064 on two).  Every step is still a whole perft
