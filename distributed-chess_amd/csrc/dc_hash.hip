@@ -62,7 +62,8 @@ enum : int {
   T_END,        // ]}}
   T_NULL,       // {"piece":null},   (the last cell of a row drops the comma)
   T_CELL0,      // {"piece":{"color":0,"kind":"P"}},  ... 12 cells: colour-major P N B R Q K
-  T_COUNT = T_CELL0 + 12
+  T_NULLRUN = T_CELL0 + 12,  // T_NULL eight times: a run of k empty cells is its first 15 k bytes
+  T_COUNT
 };
 
 constexpr JsonTpl make_json_tpl() {
@@ -70,11 +71,14 @@ constexpr JsonTpl make_json_tpl() {
   const char* strs[T_COUNT] = {"{\"turn\":", "01", ",\"white_player\":\"", "\",\"black_player\":\"",
                                "\",\"history\":\"", "\",\"board\":{\"rows\":[", "{\"cells\":[", "]},", "]}}",
                                "{\"piece\":null},", nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   int p = 0;
   for (int i = 0; i < T_COUNT; ++i) {
     t.off[i] = (uint16_t)p;
-    if (strs[i]) {
+    if (i == T_NULLRUN) {
+      for (int r = 0; r < 8; ++r)
+        for (const char* c = strs[T_NULL]; *c; ++c) t.s[p++] = *c;
+    } else if (strs[i]) {
       for (const char* c = strs[i]; *c; ++c) t.s[p++] = *c;
     } else {  // {"piece":{"color":C,"kind":"K"}},
       const int k = i - T_CELL0;
@@ -104,6 +108,15 @@ constexpr bool cells_even() {
   return true;
 }
 static_assert(cells_even(), "the 12 piece-cell templates are consecutive and of one length");
+constexpr u32 kNullRunOff = kJsonTpl.off[T_NULLRUN];
+static_assert(kJsonTpl.len[T_NULLRUN] == 8 * kCellNullLen, "eight null cells");
+static_assert(kNullRunOff + 8 * kCellNullLen + 8 <= sizeof(kJsonTpl.s), "copy8 may read 7 bytes past a piece");
+// DC_HASH_NULLRUN (round 6): a run of empty cells in a row is one piece (the
+// first 15 k bytes of T_NULLRUN), so the board's ~32 empty cells take ~10
+// trips of the fill loop instead of 32.
+#ifndef DC_HASH_NULLRUN
+#define DC_HASH_NULLRUN 1
+#endif
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
 __device__ __forceinline__ u32 kind_index(u32 code) {
@@ -332,6 +345,20 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           }
           col = stage == S_ROW ? 0u : col + 1;
           stage = S_CELL;
+#if DC_HASH_NULLRUN
+          {
+            // empty cells from col on in this row (bit 8 stops the run at the row's end)
+            const u32 occ8 = (u32)(occupied(b) >> (8 * row)) & 0xFFu;
+            const u32 run = (u32)__builtin_ctz((occ8 | 0x100u) >> col);
+            if (run) {
+              glb = false;
+              loff = kNullRunOff;
+              rem = kCellNullLen * run - (col + run == 8 ? 1u : 0u);
+              col += run - 1;  // the run's last cell
+              break;
+            }
+          }
+#endif
           const u32 nib = nibble(b, (int)(8 * row + col));
           const u32 ki = kind_index(nib >> 1);
           // the cell templates' offsets and lengths as constants (round 6:
