@@ -47,8 +47,8 @@ namespace dc {
 // ----------------------------------------------------------- JSON templates
 // All fixed strings in one blob; a piece is (offset, length) in it.
 struct JsonTpl {
-  char s[640];
-  uint16_t off[24], len[24];
+  char s[768];
+  uint16_t off[32], len[32];
 };
 enum : int {
   T_TURN = 0,   // {"turn":
@@ -63,6 +63,9 @@ enum : int {
   T_NULL,       // {"piece":null},   (the last cell of a row drops the comma)
   T_CELL0,      // {"piece":{"color":0,"kind":"P"}},  ... 12 cells: colour-major P N B R Q K
   T_NULLRUN = T_CELL0 + 12,  // T_NULL eight times: a run of k empty cells is its first 15 k bytes
+  T_BOARD_ROW,  // ","board":{"rows":[{"cells":[   (T_BOARD + T_ROW: DC_HASH_MERGE)
+  T_ROW_SEP,    // ]},{"cells":[                  (T_ROW_END + T_ROW)
+  T_LAST,       // ]}]}}                          (the last row's end + T_END)
   T_COUNT
 };
 
@@ -71,7 +74,8 @@ constexpr JsonTpl make_json_tpl() {
   const char* strs[T_COUNT] = {"{\"turn\":", "01", ",\"white_player\":\"", "\",\"black_player\":\"",
                                "\",\"history\":\"", "\",\"board\":{\"rows\":[", "{\"cells\":[", "]},", "]}}",
                                "{\"piece\":null},", nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
-                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+                               nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                               "\",\"board\":{\"rows\":[{\"cells\":[", "]},{\"cells\":[", "]}]}}"};
   int p = 0;
   for (int i = 0; i < T_COUNT; ++i) {
     t.off[i] = (uint16_t)p;
@@ -117,6 +121,13 @@ static_assert(kNullRunOff + 8 * kCellNullLen + 8 <= sizeof(kJsonTpl.s), "copy8 m
 #ifndef DC_HASH_NULLRUN
 #define DC_HASH_NULLRUN 1
 #endif
+// DC_HASH_MERGE (round 6): fewer trips of the fill loop -- the row boundaries
+// as one piece each (T_BOARD_ROW, T_ROW_SEP, T_LAST instead of two), and up to
+// two accepted moves' tokens per token piece.
+#ifndef DC_HASH_MERGE
+#define DC_HASH_MERGE 1
+#endif
+constexpr u32 kTokPerPiece = DC_HASH_MERGE ? 2 : 1;
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
 __device__ __forceinline__ u32 kind_index(u32 code) {
@@ -132,7 +143,9 @@ __device__ __forceinline__ u32 bcd_add2(u32 a) {
 }
 
 constexpr u32 kHashThreads = 256;
-constexpr u32 kTokBytes = 16;
+// one token is at most 18 bytes (" " + 10 digits + ". " + kind + file + "x" +
+// square); 36 B holds two and keeps three 256-thread blocks' LDS under 160 KB
+constexpr u32 kTokBytes = 36;
 constexpr u32 kAccPlies = 128;  // per-lane verdict bits kept from pass 1 (4 dwords of LDS)
 // DC_HASH_COPY8 (round 5): pieces whose bytes sit in LDS (templates, move
 // tokens) are copied 8 bytes a step -- eight ds_read_u8 then eight ds_write_b8
@@ -263,9 +276,10 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
         case S_HSTART:
         case S_TOKENS: {
           stage = S_TOKENS;
-          // next accepted move: apply it and write its token "[ ]N. san"
+          // the next accepted moves (up to kTokPerPiece): their tokens "[ ]N. san"
           rem = 0;
-          while (ply < n_plies && rem == 0) {
+          u32 n = 0, got = 0;
+          while (ply < n_plies && got < kTokPerPiece) {
             const u32 p = ply++;
             u32 code = 0;
             if (info) {  // kernel-uniform
@@ -280,7 +294,6 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             // info's kinds are P0 N1 B2 R3 Q4 K5 (kind_index's order; an unknown kind never moves)
             const u32 ki = info ? (code & 7u) : kind_index(nibble(b, f) >> 1);
             const bool cap = info ? (code & 8u) != 0 : ((occupied(b) >> t) & 1) != 0;
-            u32 n = 0;
             if (ntok) mytok[n++] = ' ';
             // N's decimal digits straight into the token from the BCD (round 4
             // built them in a dynamically indexed register array: 29 % of the
@@ -311,13 +324,21 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
             cur ^= 1;
             ntok += 2;
             if (bcd_ok) bcd = bcd_add2(bcd);
+            ++got;
+          }
+          if (n) {
             glb = false;
             loff = tok_off;
             rem = n;
-          }
-          if (rem == 0) {
+          } else {
+#if DC_HASH_MERGE
+            stage = S_ROW;  // the board's header and its first row's (row 0)
+            row = 0;
+            tpl_piece(T_BOARD_ROW, 0);
+#else
             stage = S_BOARD;
             tpl_piece(T_BOARD, 0);
+#endif
           }
           break;
         }
@@ -339,8 +360,19 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
         case S_ROW:
         case S_CELL: {
           if (stage == S_CELL && col == 7) {
+#if DC_HASH_MERGE
+            if (row == 7) {  // the last row's end and the board's and object's
+              stage = S_END;
+              tpl_piece(T_LAST, 0);
+            } else {  // this row's end and the next row's header
+              ++row;
+              stage = S_ROW;
+              tpl_piece(T_ROW_SEP, 0);
+            }
+#else
             stage = S_ROW_END;
             tpl_piece(T_ROW_END, row == 7 ? 1u : 0u);
+#endif
             break;
           }
           col = stage == S_ROW ? 0u : col + 1;
