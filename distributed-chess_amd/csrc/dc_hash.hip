@@ -127,6 +127,13 @@ static_assert(kNullRunOff + 8 * kCellNullLen + 8 <= sizeof(kJsonTpl.s), "copy8 m
 #ifndef DC_HASH_MERGE
 #define DC_HASH_MERGE 1
 #endif
+// DC_HASH_TOK3 (round 6): three tokens per piece while the move numbers are
+// BCD (a token then has at most 15 bytes), two otherwise; the token area grows
+// to 46 B a lane and the block rows shrink to 144 B to keep three blocks' LDS
+// under 160 KB.
+#ifndef DC_HASH_TOK3
+#define DC_HASH_TOK3 1
+#endif
 constexpr u32 kTokPerPiece = DC_HASH_MERGE ? 2 : 1;
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
@@ -145,7 +152,7 @@ __device__ __forceinline__ u32 bcd_add2(u32 a) {
 constexpr u32 kHashThreads = 256;
 // one token is at most 18 bytes (" " + 10 digits + ". " + kind + file + "x" +
 // square); 36 B holds two and keeps three 256-thread blocks' LDS under 160 KB
-constexpr u32 kTokBytes = 36;
+constexpr u32 kTokBytes = DC_HASH_TOK3 ? 46 : 36;
 constexpr u32 kAccPlies = 128;  // per-lane verdict bits kept from pass 1 (4 dwords of LDS)
 // DC_HASH_COPY8 (round 5): pieces whose bytes sit in LDS (templates, move
 // tokens) are copied 8 bytes a step -- eight ds_read_u8 then eight ds_write_b8
@@ -162,7 +169,7 @@ constexpr u32 kAccPlies = 128;  // per-lane verdict bits kept from pass 1 (4 dwo
 #ifndef DC_HASH_FUSE
 #define DC_HASH_FUSE 1
 #endif
-constexpr u32 kBlkRow = DC_HASH_COPY8 ? 152 : kKeccakRate;  // 38 dwords: 2-way banks for the u64 absorb reads
+constexpr u32 kBlkRow = DC_HASH_COPY8 ? (DC_HASH_TOK3 ? 144 : 152) : kKeccakRate;  // 152 = 38 dwords: 2-way banks for the u64 absorb reads
 
 // Stages of a lane's JSON stream (in order).
 enum : u32 {
@@ -279,7 +286,8 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           // the next accepted moves (up to kTokPerPiece): their tokens "[ ]N. san"
           rem = 0;
           u32 n = 0, got = 0;
-          while (ply < n_plies && got < kTokPerPiece) {
+          const u32 tok_max = (DC_HASH_TOK3 && bcd_ok) ? 3u : kTokPerPiece;  // kernel-uniform
+          while (ply < n_plies && got < tok_max) {
             const u32 p = ply++;
             u32 code = 0;
             if (info) {  // kernel-uniform
