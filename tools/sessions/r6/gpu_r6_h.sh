@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 6, session 3: state hash with the final boards from the info pass, BCD
-# move numbers and constant cell templates (product) against HEAD 4dc353c
+# move numbers and constant cell templates (product) against the previous commit
 # (libdchess_old.so): hash/replay-info parity, then alternating bench lines.
 export TMPDIR=/tmp
 O=gpurun_out/r6h; mkdir -p $O
