@@ -135,6 +135,14 @@ static_assert(kNullRunOff + 8 * kCellNullLen + 8 <= sizeof(kJsonTpl.s), "copy8 m
 #define DC_HASH_TOK3 1
 #endif
 constexpr u32 kTokPerPiece = DC_HASH_MERGE ? 2 : 1;
+// DC_HASH_PF (round 6): with the replay pre-pass (info), the token loop takes
+// each ply's info byte and move word from a queue of DC_HASH_PF plies loaded
+// ahead (0: loaded where used, the move's load waiting on the info byte's).
+// Same box, alternating: 4 against 0, kernel 3.26-3.29 -> 3.15-3.20 ms
+// (profiles/r06/ab_hash_pf.txt); 8 against 4 within 0.5 % (ab_hash_pf8.txt).
+#ifndef DC_HASH_PF
+#define DC_HASH_PF 4
+#endif
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
 __device__ __forceinline__ u32 kind_index(u32 code) {
@@ -253,6 +261,18 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
     wn1 = names_off[2 * g + 1];
     bn1 = names_off[2 * g + 2];
   }
+#if DC_HASH_PF
+  u32 pq_c[DC_HASH_PF], pq_m[DC_HASH_PF];  // plies ply .. ply + DC_HASH_PF - 1 (clamped to the last)
+#pragma unroll
+  for (int j = 0; j < DC_HASH_PF; ++j) {
+    pq_c[j] = pq_m[j] = 0;
+    if (info && active && n_plies) {
+      const u32 pn = min((u32)j, n_plies - 1);
+      pq_c[j] = info[(size_t)pn * n_games + g];
+      pq_m[j] = moves[(size_t)pn * n_games + g];
+    }
+  }
+#endif
   const u32 tok_off = kTplBytes + tid * kTokBytes;
   char* mytok = lpool + tok_off;
   auto tpl_piece = [&](int i, u32 drop) {
@@ -289,15 +309,32 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
           const u32 tok_max = (DC_HASH_TOK3 && bcd_ok) ? 3u : kTokPerPiece;  // kernel-uniform
           while (ply < n_plies && got < tok_max) {
             const u32 p = ply++;
-            u32 code = 0;
+            u32 code = 0, m = 0;
+#if DC_HASH_PF
             if (info) {  // kernel-uniform
-              code = info[(size_t)p * n_games + g];
+              code = pq_c[0];
+              m = pq_m[0];
+#pragma unroll
+              for (int j = 0; j + 1 < DC_HASH_PF; ++j) {
+                pq_c[j] = pq_c[j + 1];
+                pq_m[j] = pq_m[j + 1];
+              }
+              const u32 pn = min(p + DC_HASH_PF, n_plies - 1);
+              pq_c[DC_HASH_PF - 1] = info[(size_t)pn * n_games + g];
+              pq_m[DC_HASH_PF - 1] = moves[(size_t)pn * n_games + g];
               if (code == 0xFFu) continue;  // rejected
-            } else if (p < kAccPlies && ((accb[p >> 5][tid] >> (p & 31)) & 1) == 0) {
-              continue;  // rejected in pass 1
+            } else
+#endif
+            {
+              if (info) {  // kernel-uniform
+                code = info[(size_t)p * n_games + g];
+                if (code == 0xFFu) continue;  // rejected
+              } else if (p < kAccPlies && ((accb[p >> 5][tid] >> (p & 31)) & 1) == 0) {
+                continue;  // rejected in pass 1
+              }
+              m = moves[(size_t)p * n_games + g];
+              if (!info && p >= kAccPlies && (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK)) continue;
             }
-            const u32 m = moves[(size_t)p * n_games + g];
-            if (!info && p >= kAccPlies && (m == 0xFFFFu || ref_verdict(b, cur, m) != V_OK)) continue;
             const int f = (int)(m & 63), t = (int)((m >> 6) & 63);
             // info's kinds are P0 N1 B2 R3 Q4 K5 (kind_index's order; an unknown kind never moves)
             const u32 ki = info ? (code & 7u) : kind_index(nibble(b, f) >> 1);
