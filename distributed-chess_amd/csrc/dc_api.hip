@@ -135,6 +135,8 @@ struct dc_ctx {
   DBuf<dc::ResultCursor> rcur;  // dc_perft_repeat_device: where the next run's result goes
   dc::PerftResult* res_host = nullptr;  // pinned
   u64* replay_host = nullptr;            // pinned: the replay kernel's five counters
+  u32* plain_host = nullptr;             // pinned: the state hash's names check (k_names_plain's flag)
+  hipEvent_t plain_ev = nullptr;         // ... recorded after its readback
   struct HostIo* host_io = nullptr;      // pinned: small validate / apply batches, read and written in place
   uint32_t io_seq = 0;                   // last completion flag value published into host_io->done
   // dc_live_validator: the resident wave's mailbox (pinned, coherent), its
@@ -252,6 +254,8 @@ struct dc_ctx {
     if (rgraph_batch) (void)hipGraphExecDestroy(rgraph_batch);
     if (res_host) (void)hipHostFree(res_host);
     if (replay_host) (void)hipHostFree(replay_host);
+    if (plain_host) (void)hipHostFree(plain_host);
+    if (plain_ev) (void)hipEventDestroy(plain_ev);
     if (host_io) (void)hipHostFree(host_io);
     if (live) (void)hipHostFree(live);
     if (live_stream) (void)hipStreamDestroy(live_stream);
@@ -1082,11 +1086,31 @@ u32 count_ws_tokens(const char* s, size_t n) {
   return count;
 }
 
+// Enqueues the names check of stage_hash_text: k_names_plain's flag (0: no
+// byte of any name needs escaping and the offsets are ordered) is read back
+// into pinned memory, then plain_ev is recorded.  state_hash_impl enqueues it
+// ahead of the replay pre-pass, so the host's wait for the flag ends while the
+// GPU still runs the pass and the hash kernel is enqueued behind the pass
+// (round 6: a stream-wide wait after the pass left the GPU idle between the
+// two kernels).
+int begin_names_check(dc_ctx* c, const char* d_names, const uint32_t* d_names_off, uint32_t n_games) {
+  const u64 n_str = 2ull * n_games;
+  if (n_str + 1 > 0x7FFFFFFFull) return DC_EUNSUPPORTED;  // hipcub's item count is an int
+  if (!c->plain_host) HIP_TRY(hipHostMalloc((void**)&c->plain_host, sizeof(u32)));
+  if (!c->plain_ev) HIP_TRY(hipEventCreateWithFlags(&c->plain_ev, hipEventDisableTiming));
+  HIP_TRY(c->esc_lens.ensure(n_str + 1));
+  HIP_TRY(dc::launch_names_plain(c->stream, d_names, d_names_off, (u32)n_str, c->esc_lens.p));
+  HIP_TRY(hipMemcpyAsync(c->plain_host, c->esc_lens.p, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(c->plain_ev, c->stream));
+  return DC_SUCCESS;
+}
+
 // Stages the hash kernel's text on the device: hash_text = the start history
 // escaped on the host (one string per batch) followed by the player names
 // escaped on the device from the raw UTF-8 in d_names (serde_json's table,
 // k_escape_len / k_escape_write); hash_off = the names' escaped offsets.  One
-// small readback sizes hash_text from the exact escaped total.
+// small readback sizes hash_text from the exact escaped total.  Runs after
+// begin_names_check.
 int stage_hash_text(dc_ctx* c, const char* history, const char* d_names, const uint32_t* d_names_off, uint32_t n_games,
                     u32* hist_len, u32* hist_tokens, const char** names_out, const u32** off_out) {
   const size_t hn = history ? std::strlen(history) : 0;
@@ -1096,15 +1120,11 @@ int stage_hash_text(dc_ctx* c, const char* history, const char* d_names, const u
   *hist_len = (u32)c->hist_text.size();
   *hist_tokens = count_ws_tokens(history ? history : "", hn);
   const u64 n_str = 2ull * n_games;
-  if (n_str + 1 > 0x7FFFFFFFull) return DC_EUNSUPPORTED;  // hipcub's item count is an int
   // Fast path (round 6): names with no byte to escape and ordered offsets are
   // their own serde_json escapes; the hash kernel then reads them in place and
   // the escaping kernels, scan and copy (~80 us per 1M games) are skipped.
-  HIP_TRY(c->esc_lens.ensure(n_str + 1));
-  HIP_TRY(dc::launch_names_plain(c->stream, d_names, d_names_off, (u32)n_str, c->esc_lens.p));
-  u32 escapes = 1;
-  HIP_TRY(hipMemcpyAsync(&escapes, c->esc_lens.p, sizeof(u32), hipMemcpyDeviceToHost, c->stream));
-  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipEventSynchronize(c->plain_ev));
+  const u32 escapes = *c->plain_host;
   if (!escapes) {
     HIP_TRY(c->hash_text.ensure(std::max<size_t>(*hist_len, 1)));
     if (*hist_len)
@@ -1150,6 +1170,10 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
   // the hash kernel validates nothing.  Batches past the replay kernel's one
   // buffer descriptor keep the hash kernel's own validation pass.
   const uint8_t* d_info = nullptr;
+  {
+    const int e = begin_names_check(c, d_names, d_names_off, n_games);
+    if (e != DC_SUCCESS) return e;
+  }
 #ifndef DC_HASH_PRE
 #define DC_HASH_PRE 1  // (0: the round-4 single kernel, for A/B only)
 #endif
@@ -1178,8 +1202,9 @@ int state_hash_impl(dc_ctx* c, const dc_pos* start, const char* history, const c
     d_info = c->replay_info.p;
     d_boards = c->hash_boards.p;
   }
-  // the names staged after the pass is enqueued: the staging's one readback
-  // then waits on the pass's GPU time instead of idling the GPU (round 6)
+  // the names staged after the pass is enqueued: the staging waits only for the
+  // names check enqueued ahead of the pass (begin_names_check), so the hash
+  // kernel is enqueued while the GPU runs the pass (round 6)
   u32 hist_len = 0, hist_tokens = 0;
   const char* names = nullptr;
   const u32* names_off = nullptr;
