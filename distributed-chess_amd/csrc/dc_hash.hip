@@ -143,6 +143,13 @@ constexpr u32 kTokPerPiece = DC_HASH_MERGE ? 2 : 1;
 #ifndef DC_HASH_PF
 #define DC_HASH_PF 4
 #endif
+// DC_HASH_P1 (round 6): pass 1's parity of the accepted plies reads this many
+// info bytes per batch of loads (1: one load, one wait per ply).  16 against
+// 1, same box: kernel 3.155-3.185 against 3.154-3.172 ms, no difference (the
+// waits overlap other waves' Keccak-f; profiles/r06/ab_hash_p1.txt), so 1.
+#ifndef DC_HASH_P1
+#define DC_HASH_P1 1
+#endif
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
 __device__ __forceinline__ u32 kind_index(u32 code) {
@@ -212,7 +219,19 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
   // parity and pass 2 reads kind and capture from it; no ply is validated here
   u32 stm = stm0;
   if (active && info) {
-    for (u32 p = 0; p < n_plies; ++p) stm ^= (u32)(info[(size_t)p * n_games + g] != 0xFFu);
+    // DC_HASH_P1 bytes loaded before any is used (round 6: one at a time, the
+    // loop waited a memory round trip per ply, every wave of a round at once)
+    u32 p = 0;
+#if DC_HASH_P1 > 1
+    for (; p + DC_HASH_P1 <= n_plies; p += DC_HASH_P1) {
+      u32 cb[DC_HASH_P1];
+#pragma unroll
+      for (int j = 0; j < DC_HASH_P1; ++j) cb[j] = info[(size_t)(p + j) * n_games + g];
+#pragma unroll
+      for (int j = 0; j < DC_HASH_P1; ++j) stm ^= (u32)(cb[j] != 0xFFu);
+    }
+#endif
+    for (; p < n_plies; ++p) stm ^= (u32)(info[(size_t)p * n_games + g] != 0xFFu);
   } else if (active) {
     Board b = start;
     u32 bits = 0;
