@@ -132,6 +132,11 @@ __device__ __forceinline__ void keccak_f1600_dev(uint64_t* a64) {
 #ifndef DC_KECCAK_UNROLL
 #define DC_KECCAK_UNROLL 1
 #endif
+// DC_KECCAK_FUSE (round 6): theta without D (see the round body): same box,
+// alternating, hash kernel 3.18-3.20 -> 3.10-3.12 ms (profiles/r06/ab_keccak_fuse.txt).
+#ifndef DC_KECCAK_FUSE
+#define DC_KECCAK_FUSE 1
+#endif
 #pragma unroll DC_KECCAK_UNROLL
   for (int r = 0; r < 24; ++r) {
     const K64 c0 = kx3(kx3(a[0], a[5], a[10]), a[15], a[20]);
@@ -139,34 +144,60 @@ __device__ __forceinline__ void keccak_f1600_dev(uint64_t* a64) {
     const K64 c2 = kx3(kx3(a[2], a[7], a[12]), a[17], a[22]);
     const K64 c3 = kx3(kx3(a[3], a[8], a[13]), a[18], a[23]);
     const K64 c4 = kx3(kx3(a[4], a[9], a[14]), a[19], a[24]);
+#if DC_KECCAK_FUSE
+    // theta's D[x] = C[x-1] ^ rot1(C[x+1]) is never formed: each lane takes
+    // a ^ C[x-1] ^ rot1(C[x+1]) as one three-input xor (180 VALU a round, not 190)
+    const K64 r0 = krot<1>(c0), r1 = krot<1>(c1), r2 = krot<1>(c2), r3 = krot<1>(c3), r4 = krot<1>(c4);
+#define DC_KTH(i, cm, rp) kx3(a[i], cm, rp)
+#define DC_KD0 c4, r1
+#define DC_KD1 c0, r2
+#define DC_KD2 c1, r3
+#define DC_KD3 c2, r4
+#define DC_KD4 c3, r0
+#else
     const K64 d0 = kx2(c4, krot<1>(c1)), d1 = kx2(c0, krot<1>(c2)), d2 = kx2(c1, krot<1>(c3));
     const K64 d3 = kx2(c2, krot<1>(c4)), d4 = kx2(c3, krot<1>(c0));
+#define DC_KTH(i, d) kx2(a[i], d)
+#define DC_KD0 d0
+#define DC_KD1 d1
+#define DC_KD2 d2
+#define DC_KD3 d3
+#define DC_KD4 d4
+#endif
+#define DC_KT(i, D) DC_KTH(i, D)
     K64 b[25];
-    b[0] = kx2(a[0], d0);
-    b[10] = krot<1>(kx2(a[1], d1));
-    b[20] = krot<62>(kx2(a[2], d2));
-    b[5] = krot<28>(kx2(a[3], d3));
-    b[15] = krot<27>(kx2(a[4], d4));
-    b[16] = krot<36>(kx2(a[5], d0));
-    b[1] = krot<44>(kx2(a[6], d1));
-    b[11] = krot<6>(kx2(a[7], d2));
-    b[21] = krot<55>(kx2(a[8], d3));
-    b[6] = krot<20>(kx2(a[9], d4));
-    b[7] = krot<3>(kx2(a[10], d0));
-    b[17] = krot<10>(kx2(a[11], d1));
-    b[2] = krot<43>(kx2(a[12], d2));
-    b[12] = krot<25>(kx2(a[13], d3));
-    b[22] = krot<39>(kx2(a[14], d4));
-    b[23] = krot<41>(kx2(a[15], d0));
-    b[8] = krot<45>(kx2(a[16], d1));
-    b[18] = krot<15>(kx2(a[17], d2));
-    b[3] = krot<21>(kx2(a[18], d3));
-    b[13] = krot<8>(kx2(a[19], d4));
-    b[14] = krot<18>(kx2(a[20], d0));
-    b[24] = krot<2>(kx2(a[21], d1));
-    b[9] = krot<61>(kx2(a[22], d2));
-    b[19] = krot<56>(kx2(a[23], d3));
-    b[4] = krot<14>(kx2(a[24], d4));
+    b[0] = DC_KT(0, DC_KD0);
+    b[10] = krot<1>(DC_KT(1, DC_KD1));
+    b[20] = krot<62>(DC_KT(2, DC_KD2));
+    b[5] = krot<28>(DC_KT(3, DC_KD3));
+    b[15] = krot<27>(DC_KT(4, DC_KD4));
+    b[16] = krot<36>(DC_KT(5, DC_KD0));
+    b[1] = krot<44>(DC_KT(6, DC_KD1));
+    b[11] = krot<6>(DC_KT(7, DC_KD2));
+    b[21] = krot<55>(DC_KT(8, DC_KD3));
+    b[6] = krot<20>(DC_KT(9, DC_KD4));
+    b[7] = krot<3>(DC_KT(10, DC_KD0));
+    b[17] = krot<10>(DC_KT(11, DC_KD1));
+    b[2] = krot<43>(DC_KT(12, DC_KD2));
+    b[12] = krot<25>(DC_KT(13, DC_KD3));
+    b[22] = krot<39>(DC_KT(14, DC_KD4));
+    b[23] = krot<41>(DC_KT(15, DC_KD0));
+    b[8] = krot<45>(DC_KT(16, DC_KD1));
+    b[18] = krot<15>(DC_KT(17, DC_KD2));
+    b[3] = krot<21>(DC_KT(18, DC_KD3));
+    b[13] = krot<8>(DC_KT(19, DC_KD4));
+    b[14] = krot<18>(DC_KT(20, DC_KD0));
+    b[24] = krot<2>(DC_KT(21, DC_KD1));
+    b[9] = krot<61>(DC_KT(22, DC_KD2));
+    b[19] = krot<56>(DC_KT(23, DC_KD3));
+    b[4] = krot<14>(DC_KT(24, DC_KD4));
+#undef DC_KT
+#undef DC_KTH
+#undef DC_KD0
+#undef DC_KD1
+#undef DC_KD2
+#undef DC_KD3
+#undef DC_KD4
 #pragma unroll
     for (int y = 0; y < 25; y += 5) {
       a[y] = kchi(b[y], b[y + 1], b[y + 2]);
