@@ -145,10 +145,12 @@ constexpr u32 kTokPerPiece = DC_HASH_MERGE ? 2 : 1;
 #endif
 // DC_HASH_P1 (round 6): pass 1's parity of the accepted plies reads this many
 // info bytes per batch of loads (1: one load, one wait per ply).  16 against
-// 1, same box: kernel 3.155-3.185 against 3.154-3.172 ms, no difference (the
-// waits overlap other waves' Keccak-f; profiles/r06/ab_hash_p1.txt), so 1.
+// 1, same box, alternating: kernel 3.08-3.10 -> 2.92-2.95 ms
+// (profiles/r06/ab_hash_p1.txt): every wave of a round starts with this loop
+// at once, so its round trips had nothing to overlap.  40 measured slower
+// than 16 (2.97-3.02 against 2.92-2.98 ms, ab_hash_p1_40.txt).
 #ifndef DC_HASH_P1
-#define DC_HASH_P1 1
+#define DC_HASH_P1 16
 #endif
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown

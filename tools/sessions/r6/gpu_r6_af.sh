@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 6, session 3: pass 1 reads 16 info bytes per batch of loads (DC_HASH_P1=16, libdchess.so) against one a ply (libdchess_old.so).
+# Round 6, session 3: pass 1 reads 40 info bytes per batch of loads (DC_HASH_P1=40, libdchess.so) against 16 (libdchess_old.so).
 # hash/replay-info parity, then alternating bench lines.
 export TMPDIR=/tmp
-O=gpurun_out/r6ae; mkdir -p $O
+O=gpurun_out/r6af; mkdir -p $O
 NEW=$PWD/distributed-chess_amd/libdchess.so OLD=$PWD/distributed-chess_amd/libdchess_old.so
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread -k "hash or info or replay" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log
