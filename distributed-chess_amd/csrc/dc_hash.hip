@@ -152,6 +152,13 @@ constexpr u32 kTokPerPiece = DC_HASH_MERGE ? 2 : 1;
 #ifndef DC_HASH_P1
 #define DC_HASH_P1 16
 #endif
+// DC_HASH_GLB8 (round 6): pieces in global memory (the names, the start
+// history) are copied 8 loads at a time instead of one load and wait a byte.
+// Same box, alternating: kernel 2.92-2.94 ms either way (the names are ~24
+// bytes a game; profiles/r06/ab_hash_glb8.txt), so off.
+#ifndef DC_HASH_GLB8
+#define DC_HASH_GLB8 0
+#endif
 
 // kind code (dc_ref.h: P=1 N=2 K=3 X=4 B=5 R=6 Q=7) -> index in P N B R Q K; 6 = unknown
 __device__ __forceinline__ u32 kind_index(u32 code) {
@@ -496,7 +503,19 @@ __global__ __launch_bounds__(kHashThreads) void k_state_hash_ref(Board start, u3
         }
         const u32 n = min(rem, (u32)kKeccakRate - fill);
         if (glb) {
+#if DC_HASH_GLB8
+          // 8 loads issued before any store (clamped to the piece's last byte;
+          // the up to 7 bytes written past it are overwritten, as in COPY8)
+          for (u32 k = 0; k < n; k += 8) {
+            char v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = src[min(k + (u32)j, n - 1)];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) my[fill + k + j] = (uint8_t)v[j];
+          }
+#else
           for (u32 k = 0; k < n; ++k) my[fill + k] = (uint8_t)src[k];
+#endif
           src += n;
         } else {
 #if DC_HASH_COPY8
